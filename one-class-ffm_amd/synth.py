@@ -1,0 +1,250 @@
+"""Seeded synthetic inputs in the reference's text format.
+
+The reference ships no datasets, so every parity test and benchmark runs on
+inputs generated here.  Each generator returns a ``Dataset`` holding the three
+files the reference's ``train`` binary reads (``train.cpp:163-193``):
+
+* the *train* file: ``j1,j2,... fid:idx:val ...`` per user row (labels are a
+  comma-separated list of positive item ids, ``ffm.cpp:92-100``);
+* the *item* file: ``fid:idx:val ...`` per item row, no label column;
+* an optional *test* file in the train format.
+
+The same content is also kept as flat arrays (row pointers, ``fid``/``idx``/
+``val`` nodes, label lists) so the benchmark can hand rows to the C-ABI
+without going through the text parser.  Feature values are rounded to three
+decimals *before* they are stored, so parsing the text (``strtod``) and using
+the arrays give bit-identical doubles.
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+from typing import List, Optional
+
+import numpy as np
+
+
+@dataclasses.dataclass
+class Rows:
+    """Rows of one input file (mirrors ``ImpData`` before ``split_fields``)."""
+
+    xptr: np.ndarray  # uint64 [m+1]
+    fid: np.ndarray  # uint32 [nnz]
+    idx: np.ndarray  # uint64 [nnz]
+    val: np.ndarray  # float64 [nnz]
+    yptr: Optional[np.ndarray] = None  # uint64 [m+1]
+    ycol: Optional[np.ndarray] = None  # uint64 [nnz_y]
+
+    @property
+    def m(self) -> int:
+        return len(self.xptr) - 1
+
+    def lines(self) -> List[str]:
+        out = []
+        xptr, fid, idx, val = self.xptr, self.fid, self.idx, self.val
+        for i in range(self.m):
+            toks = []
+            if self.yptr is not None:
+                ys = self.ycol[self.yptr[i]:self.yptr[i + 1]]
+                toks.append(",".join(str(int(j)) for j in ys))
+            for p in range(int(xptr[i]), int(xptr[i + 1])):
+                toks.append(f"{int(fid[p])}:{int(idx[p])}:{_fmt(val[p])}")
+            out.append(" ".join(toks))
+        return out
+
+    def write(self, path: str) -> None:
+        with open(path, "w") as f:
+            for line in self.lines():
+                f.write(line)
+                f.write("\n")
+
+
+def _fmt(v: float) -> str:
+    if v == 1.0:
+        return "1"
+    return repr(float(v))
+
+
+@dataclasses.dataclass
+class Dataset:
+    name: str
+    train: Rows
+    item: Rows
+    test: Optional[Rows]
+    k: int
+    params: dict
+
+    def write(self, directory: str) -> dict:
+        os.makedirs(directory, exist_ok=True)
+        paths = {
+            "train": os.path.join(directory, f"{self.name}.tr.ffm"),
+            "item": os.path.join(directory, f"{self.name}.item.ffm"),
+        }
+        self.train.write(paths["train"])
+        self.item.write(paths["item"])
+        if self.test is not None:
+            paths["test"] = os.path.join(directory, f"{self.name}.te.ffm")
+            self.test.write(paths["test"])
+        return paths
+
+    @property
+    def n_positives(self) -> int:
+        return int(self.train.yptr[-1])
+
+
+def _build_rows(feats: List[List[tuple]], labels: Optional[List[np.ndarray]]) -> Rows:
+    m = len(feats)
+    counts = np.fromiter((len(f) for f in feats), dtype=np.uint64, count=m)
+    xptr = np.zeros(m + 1, dtype=np.uint64)
+    np.cumsum(counts, out=xptr[1:])
+    nnz = int(xptr[-1])
+    fid = np.empty(nnz, dtype=np.uint32)
+    idx = np.empty(nnz, dtype=np.uint64)
+    val = np.empty(nnz, dtype=np.float64)
+    p = 0
+    for row in feats:
+        for (a, b, c) in row:
+            fid[p], idx[p], val[p] = a, b, c
+            p += 1
+    rows = Rows(xptr, fid, idx, val)
+    if labels is not None:
+        lc = np.fromiter((len(l) for l in labels), dtype=np.uint64, count=m)
+        yptr = np.zeros(m + 1, dtype=np.uint64)
+        np.cumsum(lc, out=yptr[1:])
+        rows.yptr = yptr
+        rows.ycol = (np.concatenate(labels).astype(np.uint64) if m else np.zeros(0, np.uint64))
+    return rows
+
+
+def _fast_rows(m, fields, labels_ptr=None, labels_col=None) -> Rows:
+    """Vectorised builder: ``fields`` is a list of (fid, idx[m, c], val[m, c])."""
+    per_row = sum(f[1].shape[1] for f in fields)
+    xptr = (np.arange(m + 1, dtype=np.uint64) * np.uint64(per_row))
+    fid = np.empty((m, per_row), dtype=np.uint32)
+    idx = np.empty((m, per_row), dtype=np.uint64)
+    val = np.empty((m, per_row), dtype=np.float64)
+    c0 = 0
+    for (fi, ix, vx) in fields:
+        c = ix.shape[1]
+        fid[:, c0:c0 + c] = fi
+        idx[:, c0:c0 + c] = ix
+        val[:, c0:c0 + c] = vx
+        c0 += c
+    rows = Rows(xptr, fid.reshape(-1), idx.reshape(-1), val.reshape(-1))
+    if labels_ptr is not None:
+        rows.yptr = labels_ptr.astype(np.uint64)
+        rows.ycol = labels_col.astype(np.uint64)
+    return rows
+
+
+def tiny(seed: int = 1, m: int = 1000, n: int = 50, m_test: int = 100) -> Dataset:
+    """Config 1: 1,000 rows, fu=2 (D=30, D=20), items fv=1 (D=50), k=4."""
+    rng = np.random.default_rng(seed)
+
+    def user_rows(count):
+        f0 = rng.integers(0, 30, size=count)
+        f1 = rng.integers(0, 20, size=count)
+        v1 = np.round(rng.random(count), 3)
+        v1 = np.where(v1 == 0.0, 0.001, v1)
+        labels = []
+        for _ in range(count):
+            c = int(rng.integers(1, 6))
+            labels.append(np.sort(rng.choice(n, size=c, replace=False)))
+        feats = [[(0, int(a), 1.0), (1, int(b), float(c))] for a, b, c in zip(f0, f1, v1)]
+        return _build_rows(feats, labels)
+
+    train = user_rows(m)
+    test = user_rows(m_test)
+    item = _build_rows([[(0, j, 1.0)] for j in range(n)], None)
+    return Dataset("tiny", train, item, test, k=4,
+                   params=dict(k=4, t=20, l=1e-5, w=0.1, r=-1.0))
+
+
+def _positives(rng, m, n, mean, alpha=1.2):
+    """Per-row positive lists: max(1, floor(Exp(mean))) draws, each uniform
+    w.p. 1/2 else Lomax(alpha) (= Pareto - 1) clipped to n-1; dedup + sort."""
+    draws = np.maximum(1, np.floor(rng.exponential(mean, size=m))).astype(np.int64)
+    tot = int(draws.sum())
+    uni = rng.integers(0, n, size=tot)
+    par = np.minimum(np.floor(rng.pareto(alpha, size=tot)), n - 1).astype(np.int64)
+    pick = rng.random(tot) < 0.5
+    items = np.where(pick, uni, par)
+    row = np.repeat(np.arange(m, dtype=np.int64), draws)
+    key = np.unique(row * n + items)  # dedup + sort by (row, item)
+    r = key // n
+    c = key % n
+    ptr = np.zeros(m + 1, dtype=np.int64)
+    np.cumsum(np.bincount(r, minlength=m), out=ptr[1:])
+    return ptr, c
+
+
+def kkbox(seed: int = 7, m: int = 30755, n: int = 100000, mean: float = 120.0,
+          test_frac: float = 0.1, name: str = "kkbox") -> Dataset:
+    """Config 3 (headline): user fields listener-id (D=m, 1 nnz)
+    and context (D=120, 2 nnz); item fields song-id (D=n), artist (D=n/20),
+    genre (D=50), one nnz each; values 1; k=32, -l 4 -w 2^-7 -r -1."""
+    rng = np.random.default_rng(seed)
+    ptr, col = _positives(rng, m, n, mean)
+    ctx = np.sort(np.stack([rng.choice(120, size=2, replace=False) for _ in range(m)]), axis=1) \
+        if m <= 4096 else _two_distinct(rng, m, 120)
+    uid = np.arange(m, dtype=np.uint64)[:, None]
+    train = _fast_rows(m, [(0, uid, np.ones((m, 1))), (1, ctx.astype(np.uint64), np.ones((m, 2)))],
+                       ptr, col)
+    n_art = max(1, n // 20)
+    art = rng.integers(0, n_art, size=n).astype(np.uint64)[:, None]
+    gen = rng.integers(0, 50, size=n).astype(np.uint64)[:, None]
+    sid = np.arange(n, dtype=np.uint64)[:, None]
+    item = _fast_rows(n, [(0, sid, np.ones((n, 1))), (1, art, np.ones((n, 1))),
+                          (2, gen, np.ones((n, 1)))])
+    mt = max(1, int(m * test_frac))
+    tptr, tcol = _positives(rng, mt, n, 10.0)
+    test = _fast_rows(mt, [(0, uid[:mt], np.ones((mt, 1))),
+                           (1, ctx[:mt].astype(np.uint64), np.ones((mt, 2)))], tptr, tcol)
+    return Dataset(name, train, item, test, k=32,
+                   params=dict(k=32, t=20, l=4.0, w=0.0078125, r=-1.0))
+
+
+def kkbox_small(seed: int = 11) -> Dataset:
+    """A kkbox-shaped input small enough for the fp64 oracle in a few seconds."""
+    return kkbox(seed=seed, m=2000, n=3000, mean=30.0, name="kkbox_small")
+
+
+def kkbox_s(seed: int = 7) -> Dataset:
+    """kkbox-shape-S: m=30,000, n=20,000, mean 30."""
+    return kkbox(seed=seed, m=30000, n=20000, mean=30.0, name="kkbox_s")
+
+
+def _two_distinct(rng, m, d):
+    a = rng.integers(0, d, size=m)
+    b = rng.integers(0, d - 1, size=m)
+    b = np.where(b >= a, b + 1, b)
+    return np.stack([np.minimum(a, b), np.maximum(a, b)], axis=1)
+
+
+def general(seed: int, m: int, n: int, fu: int, fv: int, k: int, d_user=None, d_item=None,
+            nnz_user=1, mean_pos=4.0, test_rows=0, vals="ones", name="general") -> Dataset:
+    """Generic multi-field generator used by the parity tests for ragged and
+    edge-case shapes (several nnz per field, empty rows, real-valued x)."""
+    rng = np.random.default_rng(seed)
+    d_user = d_user or [max(2, m // (3 + f)) for f in range(fu)]
+    d_item = d_item or [max(2, n // (2 + f)) for f in range(fv)]
+
+    def rows(count, nfields, dims, with_labels, mean):
+        feats, labels = [], []
+        for _ in range(count):
+            row = []
+            for f in range(nfields):
+                c = int(rng.integers(0, nnz_user + 1)) if nnz_user > 1 else 1
+                for _ in range(c):
+                    v = 1.0 if vals == "ones" else float(np.round(rng.random() * 2, 3) or 0.5)
+                    row.append((f, int(rng.integers(0, dims[f])), v))
+            feats.append(row)
+            if with_labels:
+                c = max(1, int(rng.poisson(mean)))
+                labels.append(np.sort(rng.choice(n, size=min(c, n), replace=False)))
+        return _build_rows(feats, labels if with_labels else None)
+
+    train = rows(m, fu, d_user, True, mean_pos)
+    item = rows(n, fv, d_item, False, 0)
+    test = rows(test_rows, fu, d_user, True, mean_pos) if test_rows else None
+    return Dataset(name, train, item, test, k=k, params=dict(k=k, t=3, l=0.5, w=0.05, r=-1.0))

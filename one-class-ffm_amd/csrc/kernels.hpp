@@ -1,0 +1,871 @@
+// kernels.hpp — CDNA4 (gfx950) device code of the one-class FFM epoch.
+//
+// Every pass of the reference epoch (ffm.cpp:314-870) is a gather / dot /
+// AXPY over k-vectors, bound by HBM (or Infinity-Cache) bandwidth, not by
+// MFMA.  Layout: every table (W, H, P, Q, S, V, R, Hv, h) is row-major with a
+// padded row stride KP = next power of two >= k (padding columns stay exactly
+// zero, so results equal the unpadded math).  One lane owns VE consecutive
+// elements of a row (16 bytes: float4 / double2), so LPR = KP/VE lanes cover
+// a row and a 64-lane wave holds NSG = 64/LPR "subgroups".
+//
+// Row kernels run one row per wave: subgroups split the row's positives
+// (or feature nodes), each subgroup gathers whole 16-B-per-lane row slices,
+// and cross-subgroup sums use xor shuffles.  The scatter x_i (x) h_i into the
+// D x k gradient / Hessian-vector buffers is done without per-thread buffers
+// (the reference's nr_threads x D x k copies, ffm.cpp:557,759): a row pass
+// writes h (R x k), then a feature-major (CSC) pass sums each feature's rows
+// in chunks; single-chunk features are plain stores, multi-chunk features
+// (low-cardinality fields) use float atomics into a buffer that the
+// finalising pass zeroes again.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ocffm {
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef double d2v __attribute__((ext_vector_type(2)));
+
+template <typename real> struct VT;
+template <> struct VT<float> {
+  using V = f4v;
+  static constexpr int N = 4;
+};
+template <> struct VT<double> {
+  using V = d2v;
+  static constexpr int N = 2;
+};
+template <typename real> using vec_t = typename VT<real>::V;
+
+template <typename real, int KP> struct Geo {
+  static constexpr int VE = VT<real>::N;
+  static constexpr int LPR = KP / VE;  // lanes per row
+  static constexpr int NSG = 64 / LPR; // rows (subgroups) per wave
+  static_assert(LPR >= 1 && LPR <= 64, "KP out of range");
+};
+
+constexpr int BLOCK = 256;   // 4 waves
+constexpr int MAXCG = 20;    // ffm.cpp:761
+constexpr double CG_EPS = 9e-2;  // ffm.cpp:762
+
+struct Chunk {  // a run of CSC entries of one feature column
+  uint32_t col;
+  uint32_t single;  // 1: the column has exactly this chunk -> plain store
+  int64_t b, e;
+};
+
+// Device-resident CG scalars (the host never reads them on the hot path).
+struct CgState {
+  double g2, r2, alpha, beta, vhv;
+  int run[MAXCG + 2];  // run[it]: CG iteration `it` (1-based) executes
+  int nr_cg;
+  unsigned counter;    // last-block ticket of the reductions below
+  double scal[4];      // misc scalars (sum of a partner bias, ...)
+};
+
+template <typename real> __device__ __forceinline__ vec_t<real> vld(const real *p) {
+  return *reinterpret_cast<const vec_t<real> *>(p);
+}
+template <typename real> __device__ __forceinline__ void vst(real *p, vec_t<real> v) {
+  *reinterpret_cast<vec_t<real> *>(p) = v;
+}
+template <typename real> __device__ __forceinline__ vec_t<real> vzero() {
+  vec_t<real> v;
+#pragma unroll
+  for (int e = 0; e < VT<real>::N; e++) v[e] = (real)0;
+  return v;
+}
+template <typename real> __device__ __forceinline__ real hsum(vec_t<real> v) {
+  real s = v[0];
+#pragma unroll
+  for (int e = 1; e < VT<real>::N; e++) s += v[e];
+  return s;
+}
+template <typename real> __device__ __forceinline__ vec_t<real> vsplat(real x) {
+  vec_t<real> v;
+#pragma unroll
+  for (int e = 0; e < VT<real>::N; e++) v[e] = x;
+  return v;
+}
+
+// Sum over the LPR lanes of one subgroup (all of them active together).
+template <int LPR, typename T> __device__ __forceinline__ T sg_sum(T x) {
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+// Sum over the NSG subgroups of a wave (lane-wise, whole wave active).
+template <int LPR, typename T> __device__ __forceinline__ T xsg_sum(T x) {
+#pragma unroll
+  for (int o = LPR; o < 64; o <<= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+template <int LPR, typename real> __device__ __forceinline__ vec_t<real> xsg_vsum(vec_t<real> v) {
+#pragma unroll
+  for (int e = 0; e < VT<real>::N; e++) v[e] = xsg_sum<LPR>(v[e]);
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum(double x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+
+// Deterministic block sum (fixed tree), result valid in every thread.
+__device__ __forceinline__ double block_sum(double v) {
+  __shared__ double sh[BLOCK / 64];
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  double t = 0;
+#pragma unroll
+  for (int i = 0; i < BLOCK / 64; i++) t += sh[i];
+  return t;
+}
+
+// Cross-block reduction by the last-arriving block (MI355X guide G16:
+// release fence + asm vmcnt(0) before the ticket, acquire fence after).
+// Partials are summed in block order: deterministic for a fixed grid.
+template <int NV>
+__device__ __forceinline__ bool last_block(const double (&v)[NV], double *part, unsigned *counter,
+                                           double (&tot)[NV]) {
+  __shared__ int s_last;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; k++) part[(size_t)blockIdx.x * NV + k] = v[k];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = atomicAdd(counter, 1u);
+    s_last = (t == gridDim.x - 1);
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!s_last) return false;
+#pragma unroll
+  for (int k = 0; k < NV; k++) {
+    double x = 0;
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += BLOCK) x += __hip_atomic_load(&part[(size_t)b * NV + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tot[k] = block_sum(x);
+  }
+  if (threadIdx.x == 0) *counter = 0u;
+  return true;
+}
+
+#define WAVE_SETUP                                                                  \
+  const int lane = threadIdx.x & 63;                                                \
+  const uint64_t wave = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;          \
+  const uint64_t nwaves = ((uint64_t)gridDim.x * BLOCK) >> 6;                       \
+  (void)lane;                                                                       \
+  (void)nwaves;
+
+// ------------------------------------------------------------------ UTX ---
+// out_i = sum_{x in X_i} val * A[idx]  (ffm.cpp:314-331).  One row per subgroup.
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_utx(uint64_t R, const int64_t *__restrict__ xptr,
+                                               const uint32_t *__restrict__ xidx, const real *__restrict__ xval,
+                                               const real *__restrict__ A, real *__restrict__ out) {
+  using G = Geo<real, KP>;
+  WAVE_SETUP
+  const int sg = lane / G::LPR, li = lane % G::LPR;
+  for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
+    vec_t<real> acc = vzero<real>();
+    for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
+      acc += vsplat<real>(xval[p]) * vld<real>(A + (size_t)xidx[p] * KP + li * G::VE);
+    vst<real>(out + i * KP + li * G::VE, acc);
+  }
+}
+
+// acc_i += <P_i, Q_i>  (add_side, ffm.cpp:352-358).  One row per subgroup.
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_rowdot_add(uint64_t R, const real *__restrict__ P,
+                                                      const real *__restrict__ Q, real *__restrict__ acc) {
+  using G = Geo<real, KP>;
+  WAVE_SETUP
+  const int sg = lane / G::LPR, li = lane % G::LPR;
+  for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
+    const real d = sg_sum<G::LPR>(hsum<real>(vld<real>(P + i * KP + li * G::VE) * vld<real>(Q + i * KP + li * G::VE)));
+    if (li == 0) acc[i] += d;
+  }
+}
+
+// out_i = sum_c <T_c[i], v_c>  (sa / sb of cache_sasb, ffm.cpp:514-535).
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_rowdot_multi(uint64_t R, int C, const real *const *__restrict__ tabs,
+                                                        const double *__restrict__ vecs, real *__restrict__ out) {
+  using G = Geo<real, KP>;
+  WAVE_SETUP
+  const int sg = lane / G::LPR, li = lane % G::LPR;
+  for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
+    real s = 0;
+    for (int c = 0; c < C; c++) {
+      const vec_t<real> t = vld<real>(tabs[c] + i * KP + li * G::VE);
+      vec_t<real> v;
+#pragma unroll
+      for (int e = 0; e < G::VE; e++) v[e] = (real)vecs[(size_t)c * KP + li * G::VE + e];
+      s += sg_sum<G::LPR>(hsum<real>(t * v));
+    }
+    if (li == 0) out[i] = s;
+  }
+}
+
+// y~_ij = a_i + b_j + sum_c <P_c[i], Q_c[j]> - 1 for every positive, written
+// to both orientations (init_y_tilde, ffm.cpp:388-403).  One row per wave.
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_init_ytilde(uint64_t R, const int64_t *__restrict__ yptr,
+                                                       const uint32_t *__restrict__ ycol, real *__restrict__ yt,
+                                                       real *__restrict__ yt_other, const uint32_t *__restrict__ perm,
+                                                       int C, const real *const *__restrict__ Ptabs,
+                                                       const real *const *__restrict__ Qtabs,
+                                                       const real *__restrict__ a, const real *__restrict__ b) {
+  using G = Geo<real, KP>;
+  WAVE_SETUP
+  const int sg = lane / G::LPR, li = lane % G::LPR;
+  for (uint64_t i = wave; i < R; i += nwaves) {
+    const real ai = a[i];
+    for (int64_t p = yptr[i] + sg; p < yptr[i + 1]; p += G::NSG) {
+      const uint32_t j = ycol[p];
+      real s = 0;
+      for (int c = 0; c < C; c++)
+        s += sg_sum<G::LPR>(hsum<real>(vld<real>(Ptabs[c] + i * KP + li * G::VE) *
+                                       vld<real>(Qtabs[c] + (size_t)j * KP + li * G::VE)));
+      if (li == 0) {
+        const real v = ai + b[j] + s - (real)1;
+        yt[p] = v;
+        yt_other[perm[p]] = v;
+      }
+    }
+  }
+}
+
+// --------------------------------------------------------- gradient rows ---
+// h_i = pk_i + w (T_i + (a_i - r) oQ + bQ),
+// pk_i = sum_{j in pos(i)} ((1-w) y~_ij - w (1-r)) q_j,  T_i = sum_c P_c[i] M_c
+// (gd_cross row body, ffm.cpp:658-700).  M (C x KP x KP) staged in LDS.
+template <typename real, int KP, bool MLDS>
+__global__ __launch_bounds__(BLOCK) void k_gd_cross_row(uint64_t R, const int64_t *__restrict__ yptr,
+                                                        const uint32_t *__restrict__ ycol,
+                                                        const real *__restrict__ yt, const real *__restrict__ Q1,
+                                                        int C, const real *const *__restrict__ Ptabs,
+                                                        const real *__restrict__ M, const double *__restrict__ sums,
+                                                        const real *__restrict__ a1, double w, double r,
+                                                        real *__restrict__ h) {
+  using G = Geo<real, KP>;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  real *Ms = reinterpret_cast<real *>(smem_raw);
+  const real *Mp = M;
+  if (MLDS) {
+    const int tot = C * KP * KP;
+    for (int t = threadIdx.x; t < tot; t += BLOCK) Ms[t] = M[t];
+    __syncthreads();
+    Mp = Ms;
+  }
+  WAVE_SETUP
+  const int sg = lane / G::LPR, li = lane % G::LPR;
+  const real cpos = (real)(1 - w), cneg = (real)(w * (1 - r));
+  vec_t<real> oQ, bQ;
+#pragma unroll
+  for (int e = 0; e < G::VE; e++) {
+    oQ[e] = (real)sums[li * G::VE + e];
+    bQ[e] = (real)sums[KP + li * G::VE + e];
+  }
+  for (uint64_t i = wave; i < R; i += nwaves) {
+    vec_t<real> pk = vzero<real>();
+    int64_t p = yptr[i] + sg;
+    const int64_t pe = yptr[i + 1];
+    for (; p + G::NSG < pe; p += 2 * G::NSG) {
+      const uint32_t j0 = ycol[p], j1 = ycol[p + G::NSG];
+      const real s0 = cpos * yt[p] - cneg, s1 = cpos * yt[p + G::NSG] - cneg;
+      const vec_t<real> q0 = vld<real>(Q1 + (size_t)j0 * KP + li * G::VE);
+      const vec_t<real> q1 = vld<real>(Q1 + (size_t)j1 * KP + li * G::VE);
+      pk += vsplat<real>(s0) * q0;
+      pk += vsplat<real>(s1) * q1;
+    }
+    if (p < pe) pk += vsplat<real>(cpos * yt[p] - cneg) * vld<real>(Q1 + (size_t)ycol[p] * KP + li * G::VE);
+    pk = xsg_vsum<G::LPR, real>(pk);
+    vec_t<real> t = vzero<real>();
+    for (int c = 0; c < C; c++) {
+      const real *prow = Ptabs[c] + i * KP;
+      for (int e = sg; e < KP; e += G::NSG)
+        t += vsplat<real>(prow[e]) * vld<real>(Mp + ((size_t)c * KP + e) * KP + li * G::VE);
+    }
+    t = xsg_vsum<G::LPR, real>(t);
+    const real z = a1[i] - (real)r;
+    const vec_t<real> out = pk + vsplat<real>((real)w) * (t + vsplat<real>(z) * oQ + bQ);
+    if (sg == 0) vst<real>(h + i * KP + li * G::VE, out);
+  }
+}
+
+// h_i = z_i q1_i, z_i = w (n1 (a_i - r) + sum(b) + sa_i) + sum_pos ((1-w) y~ - w (1-r))
+// (gd_side row body, ffm.cpp:572-589).  One row per wave.
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_gd_side_row(uint64_t R, const int64_t *__restrict__ yptr,
+                                                       const real *__restrict__ yt, const real *__restrict__ Q1,
+                                                       const real *__restrict__ a1, const real *__restrict__ sa1,
+                                                       const double *__restrict__ bsum, double n1, double w,
+                                                       double r, real *__restrict__ h) {
+  using G = Geo<real, KP>;
+  WAVE_SETUP
+  const int sg = lane / G::LPR, li = lane % G::LPR;
+  const real cpos = (real)(1 - w), cneg = (real)(w * (1 - r));
+  const double bs = *bsum;
+  for (uint64_t i = wave; i < R; i += nwaves) {
+    real s = 0;
+    for (int64_t p = yptr[i] + lane; p < yptr[i + 1]; p += 64) s += cpos * yt[p] - cneg;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    const real z = (real)(w * (n1 * ((double)a1[i] - r) + bs + (double)sa1[i])) + s;
+    if (sg == 0) vst<real>(h + i * KP + li * G::VE, vsplat<real>(z) * vld<real>(Q1 + i * KP + li * G::VE));
+  }
+}
+
+// ------------------------------------------------ Hessian-vector rows ---
+// h_i = d_i <phi_i, q1_i> q1_i, phi_i = X_i V, d_i = (1-w)|pos(i)| + w n1
+// (hs_side row body, ffm.cpp:603-624).  One row per subgroup.
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_hs_side_row(uint64_t R, const int64_t *__restrict__ xptr,
+                                                       const uint32_t *__restrict__ xidx,
+                                                       const real *__restrict__ xval, const real *__restrict__ V,
+                                                       const int64_t *__restrict__ yptr,
+                                                       const real *__restrict__ Q1, double w, double n1,
+                                                       real *__restrict__ h, const int *__restrict__ run) {
+  using G = Geo<real, KP>;
+  if (run && !*run) return;
+  WAVE_SETUP
+  const int sg = lane / G::LPR, li = lane % G::LPR;
+  for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
+    vec_t<real> phi = vzero<real>();
+    for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
+      phi += vsplat<real>(xval[p]) * vld<real>(V + (size_t)xidx[p] * KP + li * G::VE);
+    const vec_t<real> q = vld<real>(Q1 + i * KP + li * G::VE);
+    const real z = sg_sum<G::LPR>(hsum<real>(phi * q));
+    const real d = (real)((1 - w) * (double)(yptr[i + 1] - yptr[i]) + w * n1);
+    vst<real>(h + i * KP + li * G::VE, vsplat<real>(d * z) * q);
+  }
+}
+
+// h_i = (1-w) sum_{j in pos(i)} <phi_i, q_j> q_j + w phi_i QTQ, phi_i = X_i V
+// (hs_cross row body, ffm.cpp:715-738; tau = X_i (V QTQ) = phi_i QTQ).
+// One row per wave; QTQ staged in LDS.
+template <typename real, int KP, bool MLDS>
+__global__ __launch_bounds__(BLOCK) void k_hs_cross_row(uint64_t R, const int64_t *__restrict__ xptr,
+                                                        const uint32_t *__restrict__ xidx,
+                                                        const real *__restrict__ xval, const real *__restrict__ V,
+                                                        const int64_t *__restrict__ yptr,
+                                                        const uint32_t *__restrict__ ycol,
+                                                        const real *__restrict__ Q1, const real *__restrict__ QTQ,
+                                                        double w, real *__restrict__ h, const int *__restrict__ run) {
+  using G = Geo<real, KP>;
+  if (run && !*run) return;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  real *Qs = reinterpret_cast<real *>(smem_raw);
+  real *phis = Qs + (MLDS ? KP * KP : 0);
+  const real *Qp = QTQ;
+  if (MLDS) {
+    for (int t = threadIdx.x; t < KP * KP; t += BLOCK) Qs[t] = QTQ[t];
+    __syncthreads();
+    Qp = Qs;
+  }
+  WAVE_SETUP
+  const int sg = lane / G::LPR, li = lane % G::LPR;
+  real *myphi = phis + (threadIdx.x >> 6) * KP;
+  const real cpos = (real)(1 - w);
+  for (uint64_t i = wave; i < R; i += nwaves) {
+    vec_t<real> phi = vzero<real>();
+    for (int64_t p = xptr[i] + sg; p < xptr[i + 1]; p += G::NSG)
+      phi += vsplat<real>(xval[p]) * vld<real>(V + (size_t)xidx[p] * KP + li * G::VE);
+    phi = xsg_vsum<G::LPR, real>(phi);
+    // tau = phi QTQ: subgroup sg handles rows e = sg, sg+NSG, ... of QTQ.
+    if (sg == 0) vst<real>(myphi + li * G::VE, phi);
+    __builtin_amdgcn_wave_barrier();
+    vec_t<real> tau = vzero<real>();
+    for (int e = sg; e < KP; e += G::NSG) tau += vsplat<real>(myphi[e]) * vld<real>(Qp + (size_t)e * KP + li * G::VE);
+    tau = xsg_vsum<G::LPR, real>(tau);
+    __builtin_amdgcn_wave_barrier();
+    vec_t<real> ka = vzero<real>();
+    int64_t p = yptr[i] + sg;
+    const int64_t pe = yptr[i + 1];
+    for (; p + G::NSG < pe; p += 2 * G::NSG) {
+      const uint32_t j0 = ycol[p], j1 = ycol[p + G::NSG];
+      const vec_t<real> q0 = vld<real>(Q1 + (size_t)j0 * KP + li * G::VE);
+      const vec_t<real> q1 = vld<real>(Q1 + (size_t)j1 * KP + li * G::VE);
+      const real s0 = sg_sum<G::LPR>(hsum<real>(phi * q0));
+      const real s1 = sg_sum<G::LPR>(hsum<real>(phi * q1));
+      ka += vsplat<real>(s0) * q0;
+      ka += vsplat<real>(s1) * q1;
+    }
+    if (p < pe) {
+      const vec_t<real> q0 = vld<real>(Q1 + (size_t)ycol[p] * KP + li * G::VE);
+      ka += vsplat<real>(sg_sum<G::LPR>(hsum<real>(phi * q0))) * q0;
+    }
+    ka = xsg_vsum<G::LPR, real>(ka);
+    if (sg == 0) vst<real>(h + i * KP + li * G::VE, vsplat<real>(cpos) * ka + vsplat<real>((real)w) * tau);
+  }
+}
+
+// ---------------------------------------------------------- CSC scatter ---
+// acc[col] (+)= sum_{(row,val) in chunk} val * h[row].  One chunk per subgroup.
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_csc(uint64_t nch, const Chunk *__restrict__ ch,
+                                               const uint32_t *__restrict__ crow, const real *__restrict__ cval,
+                                               const real *__restrict__ h, real *__restrict__ acc,
+                                               const int *__restrict__ run) {
+  using G = Geo<real, KP>;
+  if (run && !*run) return;
+  WAVE_SETUP
+  const int sg = lane / G::LPR, li = lane % G::LPR;
+  for (uint64_t c = wave * G::NSG + sg; c < nch; c += nwaves * G::NSG) {
+    const Chunk k = ch[c];
+    vec_t<real> s = vzero<real>();
+    int64_t p = k.b;
+    for (; p + 1 < k.e; p += 2) {
+      const vec_t<real> h0 = vld<real>(h + (size_t)crow[p] * KP + li * G::VE);
+      const vec_t<real> h1 = vld<real>(h + (size_t)crow[p + 1] * KP + li * G::VE);
+      s += vsplat<real>(cval[p]) * h0;
+      s += vsplat<real>(cval[p + 1]) * h1;
+    }
+    if (p < k.e) s += vsplat<real>(cval[p]) * vld<real>(h + (size_t)crow[p] * KP + li * G::VE);
+    real *dst = acc + (size_t)k.col * KP + li * G::VE;
+    if (k.single) {
+      vst<real>(dst, s);
+    } else {
+#pragma unroll
+      for (int e = 0; e < G::VE; e++) unsafeAtomicAdd(dst + e, s[e]);
+    }
+  }
+}
+
+// ------------------------------------------------- CG vector kernels ---
+// All operate on n vectors of VE elements (D x KP buffers); row = v / LPR.
+#define VEC_LOOP for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < nv; v += (uint64_t)gridDim.x * BLOCK)
+
+__device__ __forceinline__ void publish_run(CgState *st, int *run_host, int idx, int val) {
+  st->run[idx] = val;
+  if (run_host) __hip_atomic_store(run_host + idx, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// G = lam*freq*W + acc; acc = 0; R = -G; V = R; S = 0; g2 = |G|^2
+// (ffm.cpp:561-570 regulariser, 773-779 CG start).
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_grad_fin(uint64_t nv, const real *__restrict__ W,
+                                                    const real *__restrict__ fw, double lam, real *__restrict__ acc,
+                                                    real *__restrict__ Gout, real *__restrict__ Rv,
+                                                    real *__restrict__ Vv, real *__restrict__ Sv, CgState *st,
+                                                    double *part, int *run_host) {
+  using G = Geo<real, KP>;
+  double g2 = 0;
+  VEC_LOOP {
+    const real reg = (real)(fw ? lam * (double)fw[v / G::LPR] : lam);
+    const vec_t<real> g = vsplat<real>(reg) * vld<real>(W + v * G::VE) + vld<real>(acc + v * G::VE);
+    vst<real>(acc + v * G::VE, vzero<real>());
+    if (Gout) vst<real>(Gout + v * G::VE, g);
+    vst<real>(Rv + v * G::VE, -g);
+    vst<real>(Vv + v * G::VE, -g);
+    vst<real>(Sv + v * G::VE, vzero<real>());
+#pragma unroll
+    for (int e = 0; e < G::VE; e++) g2 += (double)g[e] * (double)g[e];
+  }
+  double bv[1] = {block_sum(g2)}, tot[1];
+  if (last_block<1>(bv, part, &st->counter, tot) && threadIdx.x == 0) {
+    st->g2 = tot[0];
+    st->r2 = tot[0];
+    st->nr_cg = 0;
+    for (int it = 0; it <= MAXCG + 1; it++) publish_run(st, run_host, it, 0);
+    publish_run(st, run_host, 1, (tot[0] * CG_EPS < tot[0]) ? 1 : 0);
+  }
+}
+
+// Hv = lam*freq*V + acc; acc = 0; alpha = r2 / <V,Hv>  (ffm.cpp:783-805).
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_hv_fin(int it, uint64_t nv, const real *__restrict__ fw, double lam,
+                                                  real *__restrict__ acc, const real *__restrict__ Vv,
+                                                  real *__restrict__ Hv, CgState *st, double *part) {
+  using G = Geo<real, KP>;
+  if (!st->run[it]) return;
+  double vhv = 0;
+  VEC_LOOP {
+    const real reg = (real)(fw ? lam * (double)fw[v / G::LPR] : lam);
+    const vec_t<real> x = vld<real>(Vv + v * G::VE);
+    const vec_t<real> hv = vsplat<real>(reg) * x + vld<real>(acc + v * G::VE);
+    vst<real>(acc + v * G::VE, vzero<real>());
+    vst<real>(Hv + v * G::VE, hv);
+#pragma unroll
+    for (int e = 0; e < G::VE; e++) vhv += (double)x[e] * (double)hv[e];
+  }
+  double bv[1] = {block_sum(vhv)}, tot[1];
+  if (last_block<1>(bv, part, &st->counter, tot) && threadIdx.x == 0) {
+    st->vhv = tot[0];
+    st->alpha = st->r2 / tot[0];
+  }
+}
+
+// S += alpha V; R -= alpha Hv; r2' = |R|^2; beta = r2'/r2  (ffm.cpp:804-809)
+// and the loop test g2*eps < r2 && it < 20 (ffm.cpp:780).
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_cg_upd(int it, uint64_t nv, const real *__restrict__ Vv,
+                                                  const real *__restrict__ Hv, real *__restrict__ Sv,
+                                                  real *__restrict__ Rv, CgState *st, double *part, int *run_host) {
+  using G = Geo<real, KP>;
+  if (!st->run[it]) return;
+  const real alpha = (real)st->alpha;
+  double r2 = 0;
+  VEC_LOOP {
+    const vec_t<real> s = vld<real>(Sv + v * G::VE) + vsplat<real>(alpha) * vld<real>(Vv + v * G::VE);
+    const vec_t<real> rr = vld<real>(Rv + v * G::VE) - vsplat<real>(alpha) * vld<real>(Hv + v * G::VE);
+    vst<real>(Sv + v * G::VE, s);
+    vst<real>(Rv + v * G::VE, rr);
+#pragma unroll
+    for (int e = 0; e < G::VE; e++) r2 += (double)rr[e] * (double)rr[e];
+  }
+  double bv[1] = {block_sum(r2)}, tot[1];
+  if (last_block<1>(bv, part, &st->counter, tot) && threadIdx.x == 0) {
+    const double gamma = st->r2;
+    st->beta = tot[0] / gamma;
+    st->r2 = tot[0];
+    st->nr_cg = it;
+    publish_run(st, run_host, it + 1, (it < MAXCG && st->g2 * CG_EPS < tot[0]) ? 1 : 0);
+  }
+}
+
+// V = beta V + R  (ffm.cpp:810-811), only when another iteration follows.
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_cg_dir(int it, uint64_t nv, real *__restrict__ Vv,
+                                                  const real *__restrict__ Rv, const CgState *st) {
+  using G = Geo<real, KP>;
+  if (!st->run[it + 1]) return;
+  const real beta = (real)st->beta;
+  VEC_LOOP {
+    vst<real>(Vv + v * G::VE, vsplat<real>(beta) * vld<real>(Vv + v * G::VE) + vld<real>(Rv + v * G::VE));
+  }
+}
+
+// W += S  (ffm.cpp:410, 441).
+template <typename real>
+__global__ __launch_bounds__(BLOCK) void k_axpy1(uint64_t nv, const real *__restrict__ S, real *__restrict__ W) {
+  VEC_LOOP {
+    vst<real>(W + v * VT<real>::N, vld<real>(W + v * VT<real>::N) + vld<real>(S + v * VT<real>::N));
+  }
+}
+
+// ------------------------------------------------------- update rows ---
+// XS_i = X_i S; P_i += XS_i; y~_ij += <XS_i, q_j> in both orientations
+// (update_cross, ffm.cpp:439-465).  One row per wave.
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_update_cross_row(uint64_t R, const int64_t *__restrict__ xptr,
+                                                            const uint32_t *__restrict__ xidx,
+                                                            const real *__restrict__ xval,
+                                                            const real *__restrict__ S, real *__restrict__ P1,
+                                                            const int64_t *__restrict__ yptr,
+                                                            const uint32_t *__restrict__ ycol,
+                                                            real *__restrict__ yt, real *__restrict__ yt_other,
+                                                            const uint32_t *__restrict__ perm,
+                                                            const real *__restrict__ Q1) {
+  using G = Geo<real, KP>;
+  WAVE_SETUP
+  const int sg = lane / G::LPR, li = lane % G::LPR;
+  for (uint64_t i = wave; i < R; i += nwaves) {
+    vec_t<real> xs = vzero<real>();
+    for (int64_t p = xptr[i] + sg; p < xptr[i + 1]; p += G::NSG)
+      xs += vsplat<real>(xval[p]) * vld<real>(S + (size_t)xidx[p] * KP + li * G::VE);
+    xs = xsg_vsum<G::LPR, real>(xs);
+    if (sg == 0) vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
+    for (int64_t p = yptr[i] + sg; p < yptr[i + 1]; p += G::NSG) {
+      const real d = sg_sum<G::LPR>(hsum<real>(xs * vld<real>(Q1 + (size_t)ycol[p] * KP + li * G::VE)));
+      if (li == 0) {
+        yt[p] += d;
+        yt_other[perm[p]] += d;
+      }
+    }
+  }
+}
+
+// XS_i = X_i S; P_i += XS_i; gap_i = <XS_i, q1_i>; a_i += gap_i;
+// y~ += gap_i over row i's positives, both orientations (update_side,
+// ffm.cpp:405-437).  One row per wave.
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_update_side_row(uint64_t R, const int64_t *__restrict__ xptr,
+                                                           const uint32_t *__restrict__ xidx,
+                                                           const real *__restrict__ xval, const real *__restrict__ S,
+                                                           real *__restrict__ P1, const real *__restrict__ Q1,
+                                                           real *__restrict__ a1, const int64_t *__restrict__ yptr,
+                                                           real *__restrict__ yt, real *__restrict__ yt_other,
+                                                           const uint32_t *__restrict__ perm) {
+  using G = Geo<real, KP>;
+  WAVE_SETUP
+  const int sg = lane / G::LPR, li = lane % G::LPR;
+  for (uint64_t i = wave; i < R; i += nwaves) {
+    vec_t<real> xs = vzero<real>();
+    for (int64_t p = xptr[i] + sg; p < xptr[i + 1]; p += G::NSG)
+      xs += vsplat<real>(xval[p]) * vld<real>(S + (size_t)xidx[p] * KP + li * G::VE);
+    xs = xsg_vsum<G::LPR, real>(xs);
+    if (sg == 0) vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
+    const real gap = sg_sum<G::LPR>(hsum<real>(xs * vld<real>(Q1 + i * KP + li * G::VE)));
+    if (lane == 0) a1[i] += gap;
+    for (int64_t p = yptr[i] + lane; p < yptr[i + 1]; p += 64) {
+      yt[p] += gap;
+      yt_other[perm[p]] += gap;
+    }
+  }
+}
+
+// ------------------------------------------------- partner aggregates ---
+// Per-block partial sums over rows j of the partner side:
+//   gram[l][e][d] = sum_j A_l[j][e] B[j][d]   (QTQ / Q_ab^T Q1, ffm.cpp:663-670,770)
+// Thread = one 4x4 (e,d) sub-tile of one l; blockIdx.y selects a range of
+// 256 sub-tiles; threads beyond the sub-tile count split the rows.
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_gram_part(uint64_t Rp, int L, const real *const *__restrict__ A,
+                                                     const real *__restrict__ B, double *__restrict__ part,
+                                                     uint64_t rows_per_block) {
+  constexpr int Q4 = (KP >= 4) ? KP / 4 : 1;
+  const int nsub_tot = L * Q4 * Q4;
+  const int sub0 = blockIdx.y * BLOCK;
+  const int nsub = min(BLOCK, nsub_tot - sub0);
+  int groups = 1;
+  while (groups * 2 * nsub <= BLOCK) groups *= 2;
+  const int t = threadIdx.x;
+  const int g = t / nsub;
+  const int sidx = t % nsub;
+  const bool active = g < groups;
+  const int sub = sub0 + sidx;
+  const int l = sub / (Q4 * Q4);
+  const int eq = (sub / Q4) % Q4;
+  const int dq = sub % Q4;
+  float4 dummy;
+  (void)dummy;
+  double acc[16];
+#pragma unroll
+  for (int x = 0; x < 16; x++) acc[x] = 0;
+  const uint64_t r0 = (uint64_t)blockIdx.x * rows_per_block;
+  const uint64_t r1 = min(Rp, r0 + rows_per_block);
+  if (active) {
+    const real *Al = A[l];
+    for (uint64_t j = r0 + g; j < r1; j += groups) {
+      real av[4], bv[4];
+#pragma unroll
+      for (int x = 0; x < 4; x++) {
+        av[x] = Al[j * KP + eq * 4 + x];
+        bv[x] = B[j * KP + dq * 4 + x];
+      }
+#pragma unroll
+      for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) acc[x * 4 + y] += (double)av[x] * (double)bv[y];
+    }
+  }
+  // combine row groups in fixed order through LDS
+  __shared__ double sh[BLOCK * 4];
+  const size_t NOUT = (size_t)L * KP * KP;
+  for (int half = 0; half < 4; half++) {
+    __syncthreads();
+    if (active) {
+#pragma unroll
+      for (int y = 0; y < 4; y++) sh[t * 4 + y] = acc[half * 4 + y];
+    }
+    __syncthreads();
+    if (active && g == 0) {
+      double s[4] = {0, 0, 0, 0};
+      for (int gg = 0; gg < groups; gg++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) s[y] += sh[(gg * nsub + sidx) * 4 + y];
+      const int e = eq * 4 + half;
+#pragma unroll
+      for (int y = 0; y < 4; y++) part[(size_t)blockIdx.x * NOUT + ((size_t)l * KP + e) * KP + dq * 4 + y] = s[y];
+    }
+  }
+}
+
+// Column sums over the partner rows: out[0:KP] = sum_j B_j,
+// out[KP:2KP] = sum_j wv_j B_j, out[2KP] = sum_j wv_j (oQ, bQ, sum b).
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_colsum_part(uint64_t Rp, const real *__restrict__ B,
+                                                       const real *__restrict__ wv, double *__restrict__ part,
+                                                       uint64_t rows_per_block) {
+  constexpr int NOUT = 2 * KP + 1;
+  constexpr int LANES = KP < BLOCK ? KP : BLOCK;
+  constexpr int GROUPS = BLOCK / LANES;
+  const int t = threadIdx.x;
+  const int c = t % LANES, g = t / LANES;
+  const uint64_t r0 = (uint64_t)blockIdx.x * rows_per_block;
+  const uint64_t r1 = min(Rp, r0 + rows_per_block);
+  double s0 = 0, s1 = 0, s2 = 0;
+  for (uint64_t j = r0 + g; j < r1; j += GROUPS) {
+    const double wj = wv ? (double)wv[j] : 0.0;
+    const double bj = B ? (double)B[j * KP + c] : 0.0;
+    s0 += bj;
+    s1 += wj * bj;
+    if (c == 0) s2 += wj;
+  }
+  __shared__ double sh[BLOCK * 3];
+  sh[t * 3] = s0;
+  sh[t * 3 + 1] = s1;
+  sh[t * 3 + 2] = s2;
+  __syncthreads();
+  if (g == 0) {
+    double a0 = 0, a1 = 0, a2 = 0;
+    for (int gg = 0; gg < GROUPS; gg++) {
+      a0 += sh[(gg * LANES + c) * 3];
+      a1 += sh[(gg * LANES + c) * 3 + 1];
+      a2 += sh[(gg * LANES + c) * 3 + 2];
+    }
+    part[(size_t)blockIdx.x * NOUT + c] = a0;
+    part[(size_t)blockIdx.x * NOUT + KP + c] = a1;
+    if (c == 0) part[(size_t)blockIdx.x * NOUT + 2 * KP] = a2;
+  }
+}
+
+// out[o] = sum_b part[b][o] in block order; optional real copy.
+template <typename real>
+__global__ __launch_bounds__(BLOCK) void k_reduce_parts(uint64_t nb, uint64_t nout, const double *__restrict__ part,
+                                                        double *__restrict__ out, real *__restrict__ out_real) {
+  const uint64_t o = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (o >= nout) return;
+  double s = 0;
+  for (uint64_t b = 0; b < nb; b++) s += part[b * nout + o];
+  if (out) out[o] = s;
+  if (out_real) out_real[o] = (real)s;
+}
+
+// ------------------------------------------------------- validation ---
+// z[r][j] = bt_j + sum_c <Pva_c[i], Qva_c[j]> for test row i = row0 + r
+// (pred_z, ffm.cpp:915-923); cold rows (no kept feature) score by train
+// popularity (ffm.cpp:975-977).
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_scores(uint64_t rows, uint64_t row0, uint64_t n, int C,
+                                                  const real *const *__restrict__ Pva,
+                                                  const real *const *__restrict__ Qva, const real *__restrict__ bt,
+                                                  const uint8_t *__restrict__ cold, const double *__restrict__ popular,
+                                                  uint64_t npop, double *__restrict__ z) {
+  const uint64_t r = blockIdx.y;
+  const uint64_t i = row0 + r;
+  double *zr = z + r * n;
+  if (cold[i]) {
+    for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (uint64_t)gridDim.x * BLOCK)
+      zr[j] = j < npop ? popular[j] : -1.0e300;
+    return;
+  }
+  for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (uint64_t)gridDim.x * BLOCK) {
+    real s = bt[j];
+    for (int c = 0; c < C; c++) {
+      const real *p = Pva[c] + i * KP;
+      const real *q = Qva[c] + j * KP;
+      real d = 0;
+#pragma unroll
+      for (int e = 0; e < KP; e++) d += p[e] * q[e];
+      s += d;
+    }
+    zr[j] = (double)s;
+  }
+}
+
+// Per test row: ploss term, then repeated argmax over z[0:max_z) with
+// z[argmax] = MIN_Z (-1000) and first-index tie-break, accumulating hits and
+// DCG/IDCG at the cut-offs 5,10,20,40,80 (validate/prec_k/ndcg,
+// ffm.cpp:982-1128).  One block per row.  out[r] = {ploss, hits[5], ndcg[5]}.
+__global__ __launch_bounds__(BLOCK) void k_rank(uint64_t rows, uint64_t row0, uint64_t n, uint64_t max_z,
+                                                double *__restrict__ z, const int64_t *__restrict__ lptr,
+                                                const uint32_t *__restrict__ lcol, const uint8_t *__restrict__ cold,
+                                                uint64_t npop, const double *__restrict__ at,
+                                                double *__restrict__ out) {
+  const uint64_t r = blockIdx.x;
+  const uint64_t i = row0 + r;
+  double *zr = z + r * n;
+  const int64_t l0 = lptr[i], l1 = lptr[i + 1];
+  const uint64_t zsize = cold[i] ? npop : n;
+  const uint64_t mz = max_z < zsize ? max_z : zsize;
+  __shared__ double s_val[BLOCK / 64];
+  __shared__ uint64_t s_idx[BLOCK / 64];
+  __shared__ uint64_t s_am;
+  // ploss
+  double pl = 0;
+  for (int64_t p = l0 + threadIdx.x; p < l1; p += BLOCK) {
+    const uint64_t j = lcol[p];
+    if (j < zsize) {
+      const double d = 1 - zr[j] - at[i];
+      pl += d * d;
+    }
+  }
+  pl = block_sum(pl);
+  const int cut[5] = {5, 10, 20, 40, 80};
+  double hits[5] = {0, 0, 0, 0, 0}, dcg[5] = {0, 0, 0, 0, 0}, idcg[5] = {0, 0, 0, 0, 0};
+  const uint64_t nlab = (uint64_t)(l1 - l0);
+  uint64_t cnt = 0;
+  for (int s = 0; s < 5; s++) {
+    while (cnt < (uint64_t)cut[s]) {
+      if (cnt >= mz) break;
+      double bv = -1.0e308;
+      uint64_t bi = ~0ULL;
+      for (uint64_t j = threadIdx.x; j < mz; j += BLOCK) {
+        const double v = zr[j];
+        if (v > bv) {  // strided scan: keeps the lowest index among equals
+          bv = v;
+          bi = j;
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(bv, o, 64);
+        const uint64_t oi = __shfl_xor(bi, o, 64);
+        if (ov > bv || (ov == bv && oi < bi)) {
+          bv = ov;
+          bi = oi;
+        }
+      }
+      __syncthreads();
+      if ((threadIdx.x & 63) == 0) {
+        s_val[threadIdx.x >> 6] = bv;
+        s_idx[threadIdx.x >> 6] = bi;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        double v = s_val[0];
+        uint64_t id = s_idx[0];
+        for (int w2 = 1; w2 < BLOCK / 64; w2++)
+          if (s_val[w2] > v || (s_val[w2] == v && s_idx[w2] < id)) {
+            v = s_val[w2];
+            id = s_idx[w2];
+          }
+        s_am = id;
+        zr[id] = -1000.0;  // MIN_Z (ffm.h:40)
+      }
+      __syncthreads();
+      const uint64_t am = s_am;
+      if (threadIdx.x == 0) {
+        bool hit = false;
+        for (uint64_t t = 0; t < nlab; t++)
+          if (lcol[l0 + t] == am) {
+            hit = true;
+            break;
+          }
+        const double g = 1.0 / log2((double)cnt + 2);
+        if (hit) {
+          hits[s] += 1;
+          dcg[s] += g;
+        }
+        if (nlab > cnt) idcg[s] += g;
+      }
+      cnt++;
+    }
+  }
+  if (threadIdx.x == 0) {
+    for (int s = 1; s < 5; s++) {
+      hits[s] += hits[s - 1];
+      dcg[s] += dcg[s - 1];
+      idcg[s] += idcg[s - 1];
+    }
+    double *o = out + r * 11;
+    o[0] = pl;
+    for (int s = 0; s < 5; s++) {
+      o[1 + s] = hits[s];
+      o[6 + s] = dcg[s] / idcg[s];
+    }
+  }
+}
+
+}  // namespace ocffm

@@ -1,0 +1,1470 @@
+// solver.hip — device-resident block Newton-CG epoch and the C ABI.
+//
+// Host C++ owns the block schedule and the data layout; every row, feature
+// and vector pass is a kernel from kernels.hpp on one HIP stream.  The CG
+// loop (ffm.cpp:780) is data-dependent: its scalars live on the device and
+// the host only learns the loop exit one iteration late (it enqueues
+// iteration it+1 before waiting for iteration it's verdict; kernels of an
+// iteration that must not run return at entry), so the GPU never idles on a
+// host round trip.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iomanip>
+#include <iostream>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "../../include/ocffm.h"
+#include "host_data.h"
+#include "kernels.hpp"
+
+namespace ocffm {
+
+// ----------------------------------------------------------------- errors
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+static thread_local std::string g_last_error;
+
+#define HIPCHK(x)                                                                                 \
+  do {                                                                                            \
+    hipError_t e_ = (x);                                                                          \
+    if (e_ != hipSuccess)                                                                         \
+      throw Error(OCFFM_E_HIP, std::string("HIP: ") + hipGetErrorString(e_) + " at " #x);         \
+  } while (0)
+#define NCCLCHK(x)                                                                                \
+  do {                                                                                            \
+    ncclResult_t r_ = (x);                                                                        \
+    if (r_ != ncclSuccess) throw Error(OCFFM_E_COMM, std::string("RCCL: ") + ncclGetErrorString(r_)); \
+  } while (0)
+
+template <typename T> struct DevBuf {
+  T *p = nullptr;
+  size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf &) = delete;
+  DevBuf &operator=(const DevBuf &) = delete;
+  DevBuf(DevBuf &&o) noexcept : p(o.p), n(o.n) {
+    o.p = nullptr;
+    o.n = 0;
+  }
+  DevBuf &operator=(DevBuf &&o) noexcept {
+    if (this != &o) {
+      release();
+      p = o.p;
+      n = o.n;
+      o.p = nullptr;
+      o.n = 0;
+    }
+    return *this;
+  }
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  void alloc(size_t count, bool zero = true) {
+    release();
+    n = count;
+    if (count == 0) return;
+    HIPCHK(hipMalloc(&p, count * sizeof(T)));
+    if (zero) HIPCHK(hipMemset(p, 0, count * sizeof(T)));
+  }
+  void upload(const T *src, size_t count) {
+    alloc(count, false);
+    if (count) HIPCHK(hipMemcpy(p, src, count * sizeof(T), hipMemcpyHostToDevice));
+  }
+  void upload(const std::vector<T> &v) { upload(v.data(), v.size()); }
+};
+
+static uint32_t block_index(uint32_t f1, uint32_t f2, uint32_t f) { return f2 + (f - 1) * f1 - f1 * (f1 - 1) / 2; }
+
+static uint32_t pad_k(uint32_t k) {
+  uint32_t kp = 4;
+  while (kp < k) kp <<= 1;
+  return kp;
+}
+
+template <class F> static void with_kp(uint32_t kp, F &&f) {
+  switch (kp) {
+    case 4: f(std::integral_constant<int, 4>()); break;
+    case 8: f(std::integral_constant<int, 8>()); break;
+    case 16: f(std::integral_constant<int, 16>()); break;
+    case 32: f(std::integral_constant<int, 32>()); break;
+    case 64: f(std::integral_constant<int, 64>()); break;
+    case 128: f(std::integral_constant<int, 128>()); break;
+    default: throw Error(OCFFM_E_ARG, "k must be in 1..128");
+  }
+}
+
+static unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap = 4096) {
+  uint64_t g = (items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+// -------------------------------------------------------------- profiling
+struct KStat {
+  uint64_t launches = 0;
+  double ms = 0, bytes = 0;
+};
+
+// ------------------------------------------------------------------- data
+template <typename real> struct DevField {
+  uint64_t D = 0, nnz = 0;
+  DevBuf<int64_t> xptr;
+  DevBuf<uint32_t> xidx;
+  DevBuf<real> xval;
+  DevBuf<uint32_t> crow;
+  DevBuf<real> cval;
+  DevBuf<Chunk> chunks;
+  DevBuf<real> freqw;  // global feature frequency (for --freq)
+};
+
+template <typename real> struct DevSide {
+  uint64_t R = 0;       // local rows
+  uint64_t R_glob = 0;  // global rows
+  uint64_t row0 = 0;
+  std::vector<std::unique_ptr<DevField<real>>> F;
+  std::vector<uint64_t> Ds;
+  uint64_t npos = 0;
+  DevBuf<int64_t> yptr;
+  DevBuf<uint32_t> ycol;
+  DevBuf<real> yt;
+  DevBuf<uint32_t> perm;  // position of the same positive in the other orientation
+  DevBuf<real> bias;      // a (users) or b (items)
+  DevBuf<real> s;         // sa or sb
+};
+
+struct Block {
+  bool used = false;
+  uint32_t f1 = 0, f2 = 0;
+};
+
+// CSC with chunks (feature-major view of one field's CSR) built on the host.
+static void build_csc(uint64_t R, uint64_t D, const int64_t *xptr, const uint32_t *xidx, const double *xval,
+                      std::vector<uint32_t> &crow, std::vector<double> &cval, std::vector<Chunk> &chunks) {
+  const uint64_t nnz = (uint64_t)xptr[R] - (uint64_t)xptr[0];
+  std::vector<uint64_t> cptr(D + 1, 0);
+  for (int64_t p = xptr[0]; p < xptr[R]; p++) cptr[xidx[p] + 1]++;
+  for (uint64_t d = 0; d < D; d++) cptr[d + 1] += cptr[d];
+  crow.assign(nnz, 0);
+  cval.assign(nnz, 0);
+  std::vector<uint64_t> cur(cptr.begin(), cptr.end() - 1);
+  for (uint64_t i = 0; i < R; i++)
+    for (int64_t p = xptr[i]; p < xptr[i + 1]; p++) {
+      const uint64_t q = cur[xidx[p]]++;
+      crow[q] = (uint32_t)i;
+      cval[q] = xval[p];
+    }
+  // chunk length: keep every subgroup's sequential sum short.
+  const uint64_t CH = 32;
+  chunks.clear();
+  for (uint64_t d = 0; d < D; d++) {
+    const uint64_t b = cptr[d], e = cptr[d + 1];
+    if (e - b <= CH) {
+      chunks.push_back(Chunk{(uint32_t)d, 1u, (int64_t)b, (int64_t)e});
+    } else {
+      for (uint64_t s = b; s < e; s += CH) chunks.push_back(Chunk{(uint32_t)d, 0u, (int64_t)s, (int64_t)std::min(e, s + CH)});
+    }
+  }
+}
+
+// ---------------------------------------------------------------- problem
+struct ProblemBase {
+  virtual ~ProblemBase() = default;
+  virtual void init() = 0;
+  virtual void one_epoch() = 0;
+  virtual void solve_block(uint32_t f1, uint32_t f2) = 0;
+  virtual void cache_sasb() = 0;
+  virtual void validate(ocffm_metrics *m) = 0;
+  virtual uint64_t get(char what, uint32_t b12, double *out, uint64_t cap) = 0;
+  virtual void set(char what, uint32_t b12, const double *in, uint64_t len) = 0;
+  virtual void grad(uint32_t f1, uint32_t f2, int half, double *out) = 0;
+  virtual void hv(uint32_t f1, uint32_t f2, int half, const double *v, double *out) = 0;
+  virtual void save_model(const std::string &path) = 0;
+  virtual void sync() = 0;
+  virtual bool has_test() const = 0;
+  virtual uint32_t nr_pass() const = 0;
+  virtual int rank() const = 0;
+  std::vector<int32_t> cg_log;
+  std::map<std::string, KStat> kstats;
+  bool profiling = false;
+  std::string prof_filter;
+  double alg_bytes = 0;
+};
+
+struct Comm {
+  int rank = 0, nranks = 1;
+  ncclComm_t nccl = nullptr;
+  ocffm_allreduce_fn host_fn = nullptr;
+  void *host_user = nullptr;
+  bool active() const { return nranks > 1 || host_fn != nullptr; }
+};
+
+template <typename real> class Problem final : public ProblemBase {
+ public:
+  Problem(const HostData &U, const HostData *Ut, const HostData &V, const ocffm_param &prm, Comm comm)
+      : prm_(prm), comm_(comm), has_test_(Ut != nullptr) {
+    HIPCHK(hipSetDevice(prm.device));
+    HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    k_ = prm.k;
+    kp_ = pad_k(k_);
+    if (k_ == 0 || k_ > 128) throw Error(OCFFM_E_ARG, "k must be in 1..128");
+    w_ = prm.omega;
+    lam_ = prm.lambda;
+    r_ = prm.r;
+    fu_ = (uint32_t)U.f;
+    fv_ = (uint32_t)V.f;
+    f_ = fu_ + fv_;
+    if (!V.transposed) throw Error(OCFFM_E_STATE, "item data must go through ocffm_data_trans_y");
+    for (uint64_t j : U.ycol)
+      if (j >= V.m) throw Error(OCFFM_E_DATA, "train label >= number of item rows (reference: out-of-bounds read)");
+    m_glob_ = U.m;
+    n_ = V.m;
+    // shard users contiguously
+    u0_ = U.m * (uint64_t)comm_.rank / (uint64_t)comm_.nranks;
+    u1_ = U.m * (uint64_t)(comm_.rank + 1) / (uint64_t)comm_.nranks;
+    build_user_side(U);
+    build_item_side(V, U);
+    if (Ut) build_test(*Ut, U);
+    popular_.upload(U.popular);
+    npop_ = U.popular.size();
+    blocks_.resize(f_ * (f_ + 1) / 2);
+    W_.resize(blocks_.size());
+    H_.resize(blocks_.size());
+    P_.resize(blocks_.size());
+    Q_.resize(blocks_.size());
+    for (uint32_t f1 = 0; f1 < f_; f1++)
+      for (uint32_t f2 = f1; f2 < f_; f2++) {
+        Block &b = blocks_[block_index(f1, f2, f_)];
+        b.f1 = f1;
+        b.f2 = f2;
+        b.used = prm_.self_side || (f1 < fu_ && f2 >= fu_);
+      }
+    // scratch
+    uint64_t Dmax = 1, Rmax = std::max<uint64_t>(U_.R, V_.R);
+    for (auto d : U_.Ds) Dmax = std::max(Dmax, d);
+    for (auto d : V_.Ds) Dmax = std::max(Dmax, d);
+    dmax_ = Dmax;
+    const size_t dk = Dmax * kp_;
+    acc_.alloc(dk);
+    G_.alloc(dk);
+    S_.alloc(dk);
+    Vd_.alloc(dk);
+    Rv_.alloc(dk);
+    Hv_.alloc(dk);
+    h_.alloc(std::max<uint64_t>(Rmax, 1) * kp_);
+    C_ = fu_ * fv_;
+    M_.alloc(std::max<uint32_t>(C_, 1) * kp_ * kp_);
+    QTQ_.alloc((size_t)kp_ * kp_);
+    sums_.alloc(2 * kp_ + 1);
+    vecs_.alloc((size_t)std::max<uint32_t>(C_, 1) * kp_);
+    part_.alloc(1 << 22, false);
+    st_.alloc(1);
+    tabs_.alloc(4 * std::max<uint32_t>(C_, 1) + 4);
+    HIPCHK(hipHostMalloc((void **)&run_host_, sizeof(int) * (MAXCG + 2), hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(run_host_, 0, sizeof(int) * (MAXCG + 2));
+    HIPCHK(hipHostGetDevicePointer((void **)&run_host_dev_, run_host_, 0));
+    if (comm_.host_fn) HIPCHK(hipHostMalloc((void **)&stage_, Dmax * kp_ * sizeof(real), hipHostMallocDefault));
+  }
+
+  ~Problem() override {
+    if (run_host_) (void)hipHostFree(run_host_);
+    if (stage_) (void)hipHostFree(stage_);
+    for (auto &e : ev_pool_) (void)hipEventDestroy(e);
+    if (stream_) (void)hipStreamDestroy(stream_);
+    if (comm_.nccl) ncclCommDestroy(comm_.nccl);
+  }
+
+  bool has_test() const override { return has_test_; }
+  uint32_t nr_pass() const override { return prm_.nr_pass; }
+  int rank() const override { return comm_.rank; }
+  void sync() override { HIPCHK(hipStreamSynchronize(stream_)); }
+
+  // --------------------------------------------------------------- init
+  // ffm.cpp:467-512.
+  void init() override {
+    const size_t rs = sizeof(real);
+    std::vector<double> host;
+    for (uint32_t f1 = 0; f1 < f_; f1++)
+      for (uint32_t f2 = f1; f2 < f_; f2++) {
+        const uint32_t b12 = block_index(f1, f2, f_);
+        if (!blocks_[b12].used) continue;
+        DevSide<real> &s1 = side(f1), &s2 = side(f2);
+        const uint32_t fi = fidx(f1), fj = fidx(f2);
+        const uint64_t D1 = s1.Ds[fi], D2 = s2.Ds[fj];
+        W_[b12].alloc(D1 * kp_);
+        H_[b12].alloc(D2 * kp_);
+        upload_table(W_[b12], D1);
+        upload_table(H_[b12], D2);
+        P_[b12].alloc(std::max<uint64_t>(s1.R, 1) * kp_);
+        Q_[b12].alloc(std::max<uint64_t>(s2.R, 1) * kp_);
+        utx(s1, fi, W_[b12].p, P_[b12].p);
+        utx(s2, fj, H_[b12].p, Q_[b12].p);
+      }
+    (void)rs;
+    (void)host;
+    // cross-table pointer lists used by the gradient / sasb / y~ kernels
+    std::vector<real *> tl(4 * std::max<uint32_t>(C_, 1) + 4, nullptr);
+    uint32_t c = 0;
+    for (uint32_t f1 = 0; f1 < fu_; f1++)
+      for (uint32_t f2 = fu_; f2 < f_; f2++, c++) {
+        const uint32_t b12 = block_index(f1, f2, f_);
+        tl[c] = P_[b12].p;            // user-side cross tables
+        tl[C_ + c] = Q_[b12].p;       // item-side cross tables
+      }
+    HIPCHK(hipMemcpy(tabs_.p, tl.data(), tl.size() * sizeof(real *), hipMemcpyHostToDevice));
+    cache_sasb();
+    if (prm_.self_side) calc_side();
+    init_y_tilde();
+    sync();
+    inited_ = true;
+  }
+
+  // ------------------------------------------------------------ epoch
+  // ffm.cpp:852-870.
+  void one_epoch() override {
+    need_init();
+    if (prm_.self_side) {
+      for (uint32_t f1 = 0; f1 < fu_; f1++)
+        for (uint32_t f2 = f1; f2 < fu_; f2++) solve_block(f1, f2);
+      for (uint32_t f1 = fu_; f1 < f_; f1++)
+        for (uint32_t f2 = f1; f2 < f_; f2++) solve_block(f1, f2);
+    }
+    for (uint32_t f1 = 0; f1 < fu_; f1++)
+      for (uint32_t f2 = fu_; f2 < f_; f2++) solve_block(f1, f2);
+    if (prm_.self_side) cache_sasb();
+    flush_prof();
+  }
+
+  void solve_block(uint32_t f1, uint32_t f2) override {
+    need_init();
+    if (f1 > f2 || f2 >= f_) throw Error(OCFFM_E_ARG, "bad block");
+    if (!blocks_[block_index(f1, f2, f_)].used) throw Error(OCFFM_E_ARG, "block not in the model (--ns)");
+    half(f1, f2, 0);
+    half(f1, f2, 1);
+  }
+
+  // ffm.cpp:514-535.  Under sharding sb is this rank's partial (it only feeds
+  // the item-side gradient, whose partial sums are all-reduced).
+  void cache_sasb() override {
+    if (C_ == 0) return;
+    std::vector<double> vec((size_t)C_ * kp_);
+    // sums over item rows of each Q_c -> sa ; over local user rows of P_c -> sb
+    for (int sidew = 0; sidew < 2; sidew++) {
+      DevSide<real> &part_side = sidew == 0 ? V_ : U_;   // rows summed
+      DevSide<real> &out_side = sidew == 0 ? U_ : V_;    // rows scored
+      for (uint32_t c = 0; c < C_; c++) {
+        real *tab = cross_tab(sidew == 0 ? 1 : 0, c);
+        colsum(part_side.R, tab, nullptr);
+        HIPCHK(hipMemcpyAsync(vecs_.p + (size_t)c * kp_, sums_.p, kp_ * sizeof(double), hipMemcpyDeviceToDevice, stream_));
+      }
+      with_kp(kp_, [&](auto K) {
+        constexpr int KP = decltype(K)::value;
+        using Gm = Geo<real, KP>;
+        const uint64_t R = out_side.R;
+        if (R == 0) return;
+        prof_launch("rowdot_multi", (double)R * (C_ * kp_ * sizeof(real) + sizeof(real)), [&] {
+          k_rowdot_multi<real, KP><<<grid_for(R, 4 * Gm::NSG), BLOCK, 0, stream_>>>(
+              R, (int)C_, (const real *const *)(tabs_.p + (sidew == 0 ? 0 : C_)), vecs_.p, out_side.s.p);
+        });
+      });
+    }
+  }
+
+  // ------------------------------------------------------- validation
+  void validate(ocffm_metrics *out) override {
+    need_init();
+    static const uint32_t cuts[5] = {5, 10, 20, 40, 80};
+    for (int s = 0; s < 5; s++) out->top_k[s] = cuts[s];
+    if (!has_test_) {
+      out->loss = 0;
+      for (int s = 0; s < 5; s++) out->prec[s] = out->ndcg[s] = 0;
+      return;
+    }
+    // projections (ffm.cpp:932-946)
+    const uint64_t mt = T_.R;
+    std::vector<DevBuf<real>> Pva(blocks_.size()), Qva(blocks_.size());
+    for (uint32_t f1 = 0; f1 < f_; f1++)
+      for (uint32_t f2 = f1; f2 < f_; f2++) {
+        const uint32_t b12 = block_index(f1, f2, f_);
+        if (!blocks_[b12].used) continue;
+        DevSide<real> &s1 = f1 < fu_ ? T_ : V_, &s2 = f2 < fu_ ? T_ : V_;
+        Pva[b12].alloc(std::max<uint64_t>(s1.R, 1) * kp_);
+        Qva[b12].alloc(std::max<uint64_t>(s2.R, 1) * kp_);
+        utx(s1, fidx(f1), W_[b12].p, Pva[b12].p);
+        utx(s2, fidx(f2), H_[b12].p, Qva[b12].p);
+      }
+    DevBuf<real> at, bt;
+    at.alloc(std::max<uint64_t>(mt, 1));
+    bt.alloc(std::max<uint64_t>(n_, 1));
+    if (prm_.self_side)
+      for (uint32_t f1 = 0; f1 < f_; f1++)
+        for (uint32_t f2 = f1; f2 < f_; f2++) {
+          if ((f1 < fu_) != (f2 < fu_)) continue;
+          const uint32_t b12 = block_index(f1, f2, f_);
+          rowdot_add(f1 < fu_ ? mt : n_, Pva[b12].p, Qva[b12].p, f1 < fu_ ? at.p : bt.p);
+        }
+    DevBuf<real *> vt;
+    std::vector<real *> tl(2 * std::max<uint32_t>(C_, 1), nullptr);
+    for (uint32_t c = 0, f1 = 0; f1 < fu_; f1++)
+      for (uint32_t f2 = fu_; f2 < f_; f2++, c++) {
+        tl[c] = Pva[block_index(f1, f2, f_)].p;
+        tl[C_ + c] = Qva[block_index(f1, f2, f_)].p;
+      }
+    vt.upload(tl);
+    DevBuf<double> rowout;
+    rowout.alloc(std::max<uint64_t>(mt, 1) * 11);
+    const uint64_t budget = 512ull << 20;
+    const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(mt, budget / (std::max<uint64_t>(n_, 1) * 8)));
+    DevBuf<double> z;
+    z.alloc(chunk * std::max<uint64_t>(n_, 1), false);
+    const uint64_t max_z = npop_;
+    for (uint64_t r0 = 0; r0 < mt; r0 += chunk) {
+      const uint64_t rows = std::min(chunk, mt - r0);
+      with_kp(kp_, [&](auto K) {
+        constexpr int KP = decltype(K)::value;
+        dim3 g(grid_for(n_, BLOCK, 64), (unsigned)rows);
+        k_scores<real, KP><<<g, BLOCK, 0, stream_>>>(rows, r0, n_, (int)C_, vt.p, vt.p + C_, bt.p, cold_.p,
+                                                     popular_.p, npop_, z.p);
+      });
+      k_rank<<<(unsigned)rows, BLOCK, 0, stream_>>>(rows, r0, n_, max_z, z.p, T_.yptr.p, T_.ycol.p, cold_.p, npop_,
+                                                    at_double(at, mt), rowout.p + r0 * 11);
+      HIPCHK(hipGetLastError());
+    }
+    std::vector<double> ro(mt * 11);
+    if (mt) HIPCHK(hipMemcpyAsync(ro.data(), rowout.p, mt * 11 * sizeof(double), hipMemcpyDeviceToHost, stream_));
+    sync();
+    std::vector<double> tot(11, 0.0);
+    for (uint64_t i = 0; i < mt; i++)
+      for (int x = 0; x < 11; x++) tot[x] += ro[i * 11 + x];
+    allreduce_host(tot.data(), tot.size());
+    const double mt_glob = (double)T_.R_glob;
+    out->loss = std::sqrt(tot[0] / mt_glob);
+    for (int s = 0; s < 5; s++) {
+      out->prec[s] = tot[1 + s] / (mt_glob * cuts[s]);
+      out->ndcg[s] = tot[6 + s] / mt_glob;
+    }
+  }
+
+  // ----------------------------------------------------------- access
+  uint64_t get(char what, uint32_t b12, double *out, uint64_t cap) override {
+    need_init();
+    const real *src = nullptr;
+    uint64_t rows = 0, cols = 1;
+    switch (what) {
+      case 'W': case 'H': case 'P': case 'Q': {
+        if (b12 >= blocks_.size() || !blocks_[b12].used) throw Error(OCFFM_E_ARG, "block not in the model");
+        const Block &b = blocks_[b12];
+        cols = k_;
+        if (what == 'W') { src = W_[b12].p; rows = side(b.f1).Ds[fidx(b.f1)]; }
+        if (what == 'H') { src = H_[b12].p; rows = side(b.f2).Ds[fidx(b.f2)]; }
+        if (what == 'P') { src = P_[b12].p; rows = side(b.f1).R; }
+        if (what == 'Q') { src = Q_[b12].p; rows = side(b.f2).R; }
+        break;
+      }
+      case 'a': src = U_.bias.p; rows = U_.R; break;
+      case 'b': src = V_.bias.p; rows = V_.R; break;
+      case 's': src = U_.s.p; rows = U_.R; break;
+      case 't': src = V_.s.p; rows = V_.R; break;
+      case 'u': src = U_.yt.p; rows = U_.npos; break;
+      case 'v': src = V_.yt.p; rows = V_.npos; break;
+      default: throw Error(OCFFM_E_ARG, "unknown state name");
+    }
+    const uint64_t count = rows * cols;
+    if (out && cap) {
+      const uint64_t stride = (cols == 1) ? 1 : kp_;
+      std::vector<real> tmp(rows * stride);
+      sync();
+      if (rows) HIPCHK(hipMemcpy(tmp.data(), src, tmp.size() * sizeof(real), hipMemcpyDeviceToHost));
+      for (uint64_t rr = 0, o = 0; rr < rows; rr++)
+        for (uint64_t cc = 0; cc < cols && o < cap; cc++, o++) out[o] = (double)tmp[rr * stride + cc];
+    }
+    return count;
+  }
+
+  void set(char what, uint32_t b12, const double *in, uint64_t len) override {
+    need_init();
+    if (b12 >= blocks_.size() || !blocks_[b12].used) throw Error(OCFFM_E_ARG, "block not in the model");
+    const Block &b = blocks_[b12];
+    const bool isW = what == 'W';
+    if (!isW && what != 'H') throw Error(OCFFM_E_ARG, "only W or H can be set");
+    const uint32_t fl = isW ? b.f1 : b.f2;
+    DevSide<real> &s = side(fl);
+    const uint64_t D = s.Ds[fidx(fl)];
+    if (len != D * k_) throw Error(OCFFM_E_ARG, "size mismatch");
+    std::vector<real> tmp(D * kp_, (real)0);
+    for (uint64_t rr = 0; rr < D; rr++)
+      for (uint32_t cc = 0; cc < k_; cc++) tmp[rr * kp_ + cc] = (real)in[rr * k_ + cc];
+    DevBuf<real> &dst = isW ? W_[b12] : H_[b12];
+    HIPCHK(hipMemcpy(dst.p, tmp.data(), tmp.size() * sizeof(real), hipMemcpyHostToDevice));
+    utx(s, fidx(fl), dst.p, isW ? P_[b12].p : Q_[b12].p);
+    sync();
+  }
+
+  void grad(uint32_t f1, uint32_t f2, int half_id, double *out) override {
+    need_init();
+    HalfCtx hc = half_ctx(f1, f2, half_id);
+    gradient(hc);
+    copy_out(G_.p, hc.D, out);
+  }
+
+  void hv(uint32_t f1, uint32_t f2, int half_id, const double *v, double *out) override {
+    need_init();
+    HalfCtx hc = half_ctx(f1, f2, half_id);
+    std::vector<real> tmp(hc.D * kp_, (real)0);
+    for (uint64_t rr = 0; rr < hc.D; rr++)
+      for (uint32_t cc = 0; cc < k_; cc++) tmp[rr * kp_ + cc] = (real)v[rr * k_ + cc];
+    HIPCHK(hipMemcpyAsync(Vd_.p, tmp.data(), tmp.size() * sizeof(real), hipMemcpyHostToDevice, stream_));
+    if (hc.cross) {  // QTQ over the partner rows (slot of this block in the Gram list)
+      gram(hc.partner->R, (int)C_, partner_tabs(hc), hc.Q1, M_.p);
+      const uint32_t c0 = cross_slot(std::min(hc.fl, hc.fo), std::max(hc.fl, hc.fo));
+      HIPCHK(hipMemcpyAsync(QTQ_.p, M_.p + (size_t)c0 * kp_ * kp_, (size_t)kp_ * kp_ * sizeof(real),
+                            hipMemcpyDeviceToDevice, stream_));
+    }
+    // force iteration 1 to run
+    CgState hs{};
+    hs.run[1] = 1;
+    hs.r2 = 1.0;
+    sync();
+    HIPCHK(hipMemcpy(st_.p, &hs, sizeof(CgState), hipMemcpyHostToDevice));
+    hv_pass(hc, 1);
+    sync();
+    copy_out(Hv_.p, hc.D, out);
+  }
+
+  // ffm.cpp:1163-1237: the reference's text model.
+  void save_model(const std::string &path) override {
+    need_init();
+    std::ofstream o(path, std::ios::out | std::ios::trunc);
+    if (!o) throw Error(OCFFM_E_IO, "cannot write " + path);
+    o << f_ << "\n" << fu_ << "\n" << fv_ << "\n" << k_ << "\n";
+    for (uint32_t i = 0; i < fu_; i++) o << U_.Ds[i] << "\n";
+    for (uint32_t i = 0; i < fv_; i++) o << V_.Ds[i] << "\n";
+    std::vector<double> buf;
+    for (uint32_t fi = 0; fi < f_; fi++)
+      for (uint32_t fj = fi; fj < f_; fj++) {
+        const uint32_t b12 = block_index(fi, fj, f_);
+        if (!blocks_[b12].used) continue;
+        for (int t = 0; t < 2; t++) {
+          const char c = t == 0 ? 'W' : 'H';
+          const uint64_t cnt = get(c, b12, nullptr, 0);
+          buf.resize(cnt);
+          get(c, b12, buf.data(), cnt);
+          const uint64_t rows = cnt / k_;
+          for (uint64_t rr = 0; rr < rows; rr++) {
+            o << c << ',' << fi << ',' << fj << ',' << rr;
+            for (uint32_t e = 0; e < k_; e++) o << " " << buf[rr * k_ + e];
+            o << "\n";
+          }
+        }
+      }
+  }
+
+ private:
+  // ------------------------------------------------------------ setup
+  void build_fields(DevSide<real> &s, const HostData &d, uint64_t r0, uint64_t r1,
+                    const std::vector<uint64_t> &Ds_glob) {
+    s.F.clear();
+    s.Ds = Ds_glob;
+    const uint64_t R = r1 - r0;
+    for (uint64_t fi = 0; fi < Ds_glob.size(); fi++) {
+      auto F = std::make_unique<DevField<real>>();
+      F->D = Ds_glob[fi];
+      std::vector<int64_t> xptr(R + 1, 0);
+      std::vector<uint32_t> xidx;
+      std::vector<double> xval;
+      if (fi < d.f) {
+        const int64_t base = d.xptr[fi][r0];
+        for (uint64_t i = 0; i <= R; i++) xptr[i] = d.xptr[fi][r0 + i] - base;
+        xidx.assign(d.xidx[fi].begin() + base, d.xidx[fi].begin() + d.xptr[fi][r1]);
+        xval.assign(d.xval[fi].begin() + base, d.xval[fi].begin() + d.xptr[fi][r1]);
+      }
+      F->nnz = xidx.size();
+      F->xptr.upload(xptr);
+      F->xidx.upload(xidx);
+      F->xval.upload(to_real(xval));
+      std::vector<uint32_t> crow;
+      std::vector<double> cval;
+      std::vector<Chunk> ch;
+      build_csc(R, F->D, xptr.data(), xidx.data(), xval.data(), crow, cval, ch);
+      F->crow.upload(crow);
+      F->cval.upload(to_real(cval));
+      F->chunks.upload(ch);
+      if (prm_.freq && fi < d.f) {  // global counts (all rows, not just this shard)
+        std::vector<double> fr(F->D, 0.0);
+        for (uint32_t x : d.xidx[fi]) fr[x] += 1;
+        F->freqw.upload(to_real(fr));
+      }
+      s.F.push_back(std::move(F));
+    }
+  }
+
+  void build_user_side(const HostData &U) {
+    U_.R = u1_ - u0_;
+    U_.R_glob = U.m;
+    U_.row0 = u0_;
+    build_fields(U_, U, u0_, u1_, U.Ds);
+    const uint64_t pb = U.yptr[u0_], pe = U.yptr[u1_];
+    std::vector<int64_t> yptr(U_.R + 1);
+    for (uint64_t i = 0; i <= U_.R; i++) yptr[i] = (int64_t)(U.yptr[u0_ + i] - pb);
+    std::vector<uint32_t> ycol(pe - pb);
+    for (uint64_t p = pb; p < pe; p++) ycol[p - pb] = (uint32_t)U.ycol[p];
+    U_.npos = pe - pb;
+    U_.yptr.upload(yptr);
+    U_.ycol.upload(ycol);
+    U_.yt.alloc(std::max<uint64_t>(U_.npos, 1));
+    U_.bias.alloc(std::max<uint64_t>(U_.R, 1));
+    U_.s.alloc(std::max<uint64_t>(U_.R, 1));
+  }
+
+  // Item-major positives restricted to this rank's users, and the position
+  // maps between the two orientations (transY order: users increasing,
+  // labels in file order, ffm.cpp:259-294).
+  void build_item_side(const HostData &V, const HostData &U) {
+    V_.R = V.m;
+    V_.R_glob = V.m;
+    V_.row0 = 0;
+    build_fields(V_, V, 0, V.m, V.Ds);
+    std::vector<int64_t> vptr(V.m + 1, 0);
+    for (uint64_t i = u0_; i < u1_; i++)
+      for (uint64_t p = U.yptr[i]; p < U.yptr[i + 1]; p++) vptr[U.ycol[p] + 1]++;
+    for (uint64_t j = 0; j < V.m; j++) vptr[j + 1] += vptr[j];
+    const uint64_t np = (uint64_t)vptr[V.m];
+    std::vector<uint32_t> vcol(np), u2v(U_.npos), v2u(np);
+    std::vector<int64_t> cur(vptr.begin(), vptr.end() - 1);
+    const uint64_t pb = U.yptr[u0_];
+    for (uint64_t i = u0_; i < u1_; i++)
+      for (uint64_t p = U.yptr[i]; p < U.yptr[i + 1]; p++) {
+        const uint64_t q = (uint64_t)cur[U.ycol[p]]++;
+        vcol[q] = (uint32_t)(i - u0_);
+        u2v[p - pb] = (uint32_t)q;
+        v2u[q] = (uint32_t)(p - pb);
+      }
+    V_.npos = np;
+    V_.yptr.upload(vptr);
+    V_.ycol.upload(vcol);
+    V_.yt.alloc(std::max<uint64_t>(np, 1));
+    V_.perm.upload(v2u);
+    U_.perm.upload(u2v);
+    V_.bias.alloc(std::max<uint64_t>(V_.R, 1));
+    V_.s.alloc(std::max<uint64_t>(V_.R, 1));
+  }
+
+  void build_test(const HostData &Ut, const HostData &U) {
+    const uint64_t t0 = Ut.m * (uint64_t)comm_.rank / (uint64_t)comm_.nranks;
+    const uint64_t t1 = Ut.m * (uint64_t)(comm_.rank + 1) / (uint64_t)comm_.nranks;
+    T_.R = t1 - t0;
+    T_.R_glob = Ut.m;
+    T_.row0 = t0;
+    std::vector<uint64_t> Ds(U.Ds);  // test fields use the train Ds
+    build_fields(T_, Ut, t0, t1, Ds);
+    std::vector<int64_t> lptr(T_.R + 1);
+    const uint64_t lb = Ut.yptr[t0];
+    for (uint64_t i = 0; i <= T_.R; i++) lptr[i] = (int64_t)(Ut.yptr[t0 + i] - lb);
+    std::vector<uint32_t> lcol(Ut.yptr[t1] - lb);
+    for (uint64_t p = lb; p < Ut.yptr[t1]; p++)
+      lcol[p - lb] = (uint32_t)std::min<uint64_t>(Ut.ycol[p], 0xffffffffu);
+    T_.yptr.upload(lptr);
+    T_.ycol.upload(lcol);
+    std::vector<uint8_t> cold(std::max<uint64_t>(T_.R, 1), 0);
+    for (uint64_t i = 0; i < T_.R; i++) cold[i] = Ut.nnx[t0 + i] == 0;
+    cold_.upload(cold);
+  }
+
+  std::vector<real> to_real(const std::vector<double> &v) {
+    std::vector<real> o(v.size());
+    for (size_t i = 0; i < v.size(); i++) o[i] = (real)v[i];
+    return o;
+  }
+
+  void upload_table(DevBuf<real> &t, uint64_t D) {
+    std::vector<double> host(D * k_);
+    init_table(host.data(), D, k_);
+    std::vector<real> pad(D * kp_, (real)0);
+    for (uint64_t rr = 0; rr < D; rr++)
+      for (uint32_t cc = 0; cc < k_; cc++) pad[rr * kp_ + cc] = (real)host[rr * k_ + cc];
+    HIPCHK(hipMemcpy(t.p, pad.data(), pad.size() * sizeof(real), hipMemcpyHostToDevice));
+  }
+
+  void copy_out(const real *src, uint64_t D, double *out) {
+    std::vector<real> tmp(D * kp_);
+    sync();
+    HIPCHK(hipMemcpy(tmp.data(), src, tmp.size() * sizeof(real), hipMemcpyDeviceToHost));
+    for (uint64_t rr = 0; rr < D; rr++)
+      for (uint32_t cc = 0; cc < k_; cc++) out[rr * k_ + cc] = (double)tmp[rr * kp_ + cc];
+  }
+
+  void need_init() const {
+    if (!inited_) throw Error(OCFFM_E_STATE, "call ocffm_problem_init first");
+  }
+
+  DevSide<real> &side(uint32_t fl) { return fl < fu_ ? U_ : V_; }
+  uint32_t fidx(uint32_t fl) const { return fl < fu_ ? fl : fl - fu_; }
+  // cross tables: which 0 = user-side P_c, 1 = item-side Q_c (c in block order)
+  real *cross_tab(int which, uint32_t c) {
+    uint32_t cc = 0;
+    for (uint32_t f1 = 0; f1 < fu_; f1++)
+      for (uint32_t f2 = fu_; f2 < f_; f2++, cc++)
+        if (cc == c) return which == 0 ? P_[block_index(f1, f2, f_)].p : Q_[block_index(f1, f2, f_)].p;
+    return nullptr;
+  }
+  uint32_t cross_slot(uint32_t f1, uint32_t f2) const { return f1 * fv_ + (f2 - fu_); }
+  // Device list of the partner side's cross tables: a user half multiplies
+  // item-side Q_c (slots C..2C), an item half user-side P_c (slots 0..C).
+  template <class HC> const real *const *partner_tabs(const HC &h) const {
+    return (const real *const *)(tabs_.p + (h.user ? C_ : 0));
+  }
+
+  // ------------------------------------------------------ primitives
+  template <class L> void prof_launch(const char *name, double bytes, L &&launch) {
+    if (!profiling || (!prof_filter.empty() && prof_filter != name)) {
+      launch();
+      HIPCHK(hipGetLastError());
+      return;
+    }
+    hipEvent_t a = ev(), b = ev();
+    HIPCHK(hipEventRecord(a, stream_));
+    launch();
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(b, stream_));
+    pending_.push_back({name, bytes, a, b});
+  }
+  hipEvent_t ev() {
+    if (ev_free_.empty()) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      ev_pool_.push_back(e);
+      return e;
+    }
+    hipEvent_t e = ev_free_.back();
+    ev_free_.pop_back();
+    return e;
+  }
+  void flush_prof() {
+    if (pending_.empty()) return;
+    sync();
+    for (auto &p : pending_) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, p.a, p.b));
+      KStat &k = kstats[p.name];
+      k.launches++;
+      k.ms += ms;
+      k.bytes += p.bytes;
+      ev_free_.push_back(p.a);
+      ev_free_.push_back(p.b);
+    }
+    pending_.clear();
+  }
+
+  void utx(DevSide<real> &s, uint32_t fi, const real *A, real *out) {
+    if (s.R == 0) return;
+    DevField<real> &F = *s.F[fi];
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      using Gm = Geo<real, KP>;
+      prof_launch("utx", 0, [&] {
+        k_utx<real, KP><<<grid_for(s.R, 4 * Gm::NSG), BLOCK, 0, stream_>>>(s.R, F.xptr.p, F.xidx.p, F.xval.p, A, out);
+      });
+    });
+  }
+
+  void rowdot_add(uint64_t R, const real *P, const real *Q, real *acc) {
+    if (R == 0) return;
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      using Gm = Geo<real, KP>;
+      k_rowdot_add<real, KP><<<grid_for(R, 4 * Gm::NSG), BLOCK, 0, stream_>>>(R, P, Q, acc);
+      HIPCHK(hipGetLastError());
+    });
+  }
+
+  // calc_side (ffm.cpp:360-373): a += <P,Q> over user-side blocks, b over item-side.
+  void calc_side() {
+    for (uint32_t f1 = 0; f1 < f_; f1++)
+      for (uint32_t f2 = f1; f2 < f_; f2++) {
+        if ((f1 < fu_) != (f2 < fu_)) continue;
+        const uint32_t b12 = block_index(f1, f2, f_);
+        DevSide<real> &s = side(f1);
+        rowdot_add(s.R, P_[b12].p, Q_[b12].p, s.bias.p);
+      }
+  }
+
+  void init_y_tilde() {
+    if (U_.R == 0) return;
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      k_init_ytilde<real, KP><<<grid_for(U_.R, 4), BLOCK, 0, stream_>>>(
+          U_.R, U_.yptr.p, U_.ycol.p, U_.yt.p, V_.yt.p, U_.perm.p, (int)C_, (const real *const *)tabs_.p,
+          (const real *const *)(tabs_.p + C_), U_.bias.p, V_.bias.p);
+      HIPCHK(hipGetLastError());
+    });
+  }
+
+  // Column sums over Rp partner rows: sums_[0:KP] = sum B, [KP:2KP] = sum wv*B, [2KP] = sum wv.
+  void colsum(uint64_t Rp, const real *B, const real *wv) {
+    const uint64_t rpb = std::max<uint64_t>(256, (Rp + 255) / 256);
+    const unsigned nb = (unsigned)std::max<uint64_t>(1, (Rp + rpb - 1) / rpb);
+    const uint64_t nout = 2 * kp_ + 1;
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      prof_launch("colsum", (double)Rp * ((B ? kp_ : 0) + (wv ? 1 : 0)) * sizeof(real), [&] {
+        k_colsum_part<real, KP><<<nb, BLOCK, 0, stream_>>>(Rp, B, wv, part_.p, rpb);
+      });
+    });
+    k_reduce_parts<real><<<grid_for(nout, BLOCK), BLOCK, 0, stream_>>>(nb, nout, part_.p, sums_.p, nullptr);
+    HIPCHK(hipGetLastError());
+  }
+
+  // out (L x KP x KP, real) = A_l^T B over Rp partner rows; dev_list is a
+  // device array of L table pointers.
+  void gram(uint64_t Rp, int L, const real *const *dev_list, const real *B, real *out) {
+    const int Q4 = kp_ / 4;
+    const int nsub = L * Q4 * Q4;
+    const unsigned gy = (unsigned)((nsub + BLOCK - 1) / BLOCK);
+    const uint64_t nout = (uint64_t)L * kp_ * kp_;
+    uint64_t nbx = std::min<uint64_t>(256 / std::max<unsigned>(gy, 1) + 1, (Rp + 63) / 64);
+    nbx = std::max<uint64_t>(1, std::min<uint64_t>(nbx, part_.n / std::max<uint64_t>(nout, 1)));
+    const uint64_t rpb = (Rp + nbx - 1) / nbx;
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      prof_launch("gram", (double)Rp * (L + 1) * kp_ * sizeof(real), [&] {
+        k_gram_part<real, KP><<<dim3((unsigned)nbx, gy), BLOCK, 0, stream_>>>(Rp, L, dev_list, B, part_.p, rpb);
+      });
+    });
+    k_reduce_parts<real><<<grid_for(nout, BLOCK), BLOCK, 0, stream_>>>(nbx, nout, part_.p, nullptr, out);
+    HIPCHK(hipGetLastError());
+  }
+
+  // CSC scatter of h into acc over one field, then the all-reduce (if any).
+  void scatter(DevField<real> &F, const int *run) {
+    const uint64_t nch = F.chunks.n;
+    if (nch) {
+      with_kp(kp_, [&](auto K) {
+        constexpr int KP = decltype(K)::value;
+        using Gm = Geo<real, KP>;
+        const double bytes = (double)F.nnz * (4 + sizeof(real)) + (double)F.nnz * kp_ * sizeof(real) +
+                             (double)F.D * kp_ * sizeof(real) + (double)nch * sizeof(Chunk);
+        prof_launch("csc_scatter", bytes, [&] {
+          k_csc<real, KP><<<grid_for(nch, 4 * Gm::NSG), BLOCK, 0, stream_>>>(nch, F.chunks.p, F.crow.p, F.cval.p,
+                                                                             h_.p, acc_.p, run);
+        });
+      });
+    }
+    allreduce_dev(acc_.p, F.D * kp_);
+  }
+
+  void allreduce_dev(real *buf, uint64_t count) {
+    if (!comm_.active()) return;
+    if (comm_.nccl) {
+      NCCLCHK(ncclAllReduce(buf, buf, count, std::is_same<real, double>::value ? ncclDouble : ncclFloat, ncclSum,
+                            comm_.nccl, stream_));
+    } else {
+      HIPCHK(hipMemcpyAsync(stage_, buf, count * sizeof(real), hipMemcpyDeviceToHost, stream_));
+      sync();
+      if (comm_.host_fn(stage_, count, std::is_same<real, double>::value, comm_.host_user) != 0)
+        throw Error(OCFFM_E_COMM, "host all-reduce callback failed");
+      HIPCHK(hipMemcpyAsync(buf, stage_, count * sizeof(real), hipMemcpyHostToDevice, stream_));
+    }
+  }
+
+  void allreduce_host(double *buf, uint64_t count) {
+    if (!comm_.active()) return;
+    if (comm_.nccl) {
+      DevBuf<double> d;
+      d.upload(buf, count);
+      NCCLCHK(ncclAllReduce(d.p, d.p, count, ncclDouble, ncclSum, comm_.nccl, stream_));
+      HIPCHK(hipMemcpyAsync(buf, d.p, count * sizeof(double), hipMemcpyDeviceToHost, stream_));
+      sync();
+    } else if (comm_.host_fn(buf, count, 1, comm_.host_user) != 0) {
+      throw Error(OCFFM_E_COMM, "host all-reduce callback failed");
+    }
+  }
+
+  const double *at_double(DevBuf<real> &at, uint64_t mt) {
+    at_d_.alloc(std::max<uint64_t>(mt, 1));
+    if (mt) {
+      std::vector<real> t(mt);
+      HIPCHK(hipMemcpyAsync(t.data(), at.p, mt * sizeof(real), hipMemcpyDeviceToHost, stream_));
+      sync();
+      std::vector<double> d(t.begin(), t.end());
+      HIPCHK(hipMemcpy(at_d_.p, d.data(), mt * sizeof(double), hipMemcpyHostToDevice));
+    }
+    return at_d_.p;
+  }
+
+  // ------------------------------------------------------------- halves
+  struct HalfCtx {
+    uint32_t b12, fl, fo;
+    bool cross, user;
+    DevSide<real> *own, *partner;
+    DevField<real> *F;
+    uint64_t D;
+    real *W1, *P1, *Q1;
+    const real *fw;
+  };
+
+  HalfCtx half_ctx(uint32_t f1, uint32_t f2, int which) {
+    HalfCtx h;
+    h.b12 = block_index(f1, f2, f_);
+    if (!blocks_[h.b12].used) throw Error(OCFFM_E_ARG, "block not in the model (--ns)");
+    h.fl = which == 0 ? f1 : f2;
+    h.fo = which == 0 ? f2 : f1;
+    h.user = h.fl < fu_;
+    h.cross = (f1 < fu_) != (f2 < fu_);
+    h.own = &side(h.fl);
+    h.partner = h.cross ? &side(h.fo) : h.own;
+    h.F = h.own->F[fidx(h.fl)].get();
+    h.D = h.F->D;
+    h.W1 = which == 0 ? W_[h.b12].p : H_[h.b12].p;
+    h.P1 = which == 0 ? P_[h.b12].p : Q_[h.b12].p;
+    h.Q1 = which == 0 ? Q_[h.b12].p : P_[h.b12].p;
+    h.fw = prm_.freq ? h.F->freqw.p : nullptr;
+    return h;
+  }
+
+  // gd_side / gd_cross (ffm.cpp:537-703) -> G, and the CG start vectors.
+  void gradient(HalfCtx &h) {
+    DevSide<real> &own = *h.own;
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      using Gm = Geo<real, KP>;
+      const double rs = sizeof(real);
+      if (h.cross) {
+        DevSide<real> &ps = *h.partner;
+        // partner aggregates: M_c = A_c^T Q1 for every cross block (A_c = partner-side tables)
+        gram(ps.R, (int)C_, partner_tabs(h), h.Q1, M_.p);
+        colsum(ps.R, h.Q1, ps.bias.p);  // oQ, bQ
+        const size_t msz = (size_t)C_ * KP * KP * sizeof(real);
+        const bool lds = msz <= 64 * 1024;
+        const double bytes = (double)own.R * 8 + (double)own.npos * (4 + rs) + (double)ps.R * KP * rs +
+                             (double)C_ * own.R * KP * rs + (double)own.R * rs + (double)own.R * KP * rs;
+        prof_launch("gd_cross_row", bytes, [&] {
+          if (lds)
+            k_gd_cross_row<real, KP, true><<<grid_for(own.R, 4), BLOCK, msz, stream_>>>(
+                own.R, own.yptr.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
+                (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, w_, r_, h_.p);
+          else
+            k_gd_cross_row<real, KP, false><<<grid_for(own.R, 4), BLOCK, 0, stream_>>>(
+                own.R, own.yptr.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
+                (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, w_, r_, h_.p);
+        });
+        // QTQ for CG = M of this block
+        const uint32_t c0 = cross_slot(std::min(h.fl, h.fo), std::max(h.fl, h.fo));
+        HIPCHK(hipMemcpyAsync(QTQ_.p, M_.p + (size_t)c0 * KP * KP, (size_t)KP * KP * sizeof(real),
+                              hipMemcpyDeviceToDevice, stream_));
+      } else {
+        DevSide<real> &other = h.user ? V_ : U_;  // sum of the other side's bias (b_sum, ffm.cpp:551)
+        colsum(other.R, nullptr, other.bias.p);
+        const double n1 = (double)other.R;
+        const double bytes = (double)own.R * 8 + (double)own.npos * rs + (double)own.R * KP * rs * 2 +
+                             (double)own.R * rs * 2;
+        prof_launch("gd_side_row", bytes, [&] {
+          k_gd_side_row<real, KP><<<grid_for(own.R, 4), BLOCK, 0, stream_>>>(
+              own.R, own.yptr.p, own.yt.p, h.Q1, own.bias.p, own.s.p, sums_.p + 2 * KP, n1, w_, r_, h_.p);
+        });
+      }
+      scatter(*h.F, nullptr);
+      const uint64_t nv = h.D * KP / Gm::VE;
+      prof_launch("grad_fin", (double)h.D * KP * rs * 7, [&] {
+        k_grad_fin<real, KP><<<grid_for(nv, BLOCK, 2048), BLOCK, 0, stream_>>>(
+            nv, h.W1, h.fw, lam_, acc_.p, G_.p, Rv_.p, Vd_.p, S_.p, st_.p, part_.p, run_host_dev_);
+      });
+    });
+  }
+
+  // One Hessian-vector product lam*V + H(V) into Hv_ (+ alpha) for CG iteration `it`.
+  void hv_pass(HalfCtx &h, int it) {
+    DevSide<real> &own = *h.own;
+    const int *run = &st_.p->run[it];
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      using Gm = Geo<real, KP>;
+      const double rs = sizeof(real);
+      DevField<real> &F = *h.F;
+      if (own.R) {
+        if (h.cross) {
+          const size_t qsz = (size_t)KP * KP * sizeof(real);
+          const bool lds = qsz <= 32 * 1024;
+          const size_t smem = (lds ? qsz : 0) + 4 * KP * sizeof(real);
+          const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
+                               (double)own.npos * 4 + (double)h.partner->R * KP * rs + (double)own.R * KP * rs;
+          prof_launch("hs_cross_row", bytes, [&] {
+            if (lds)
+              k_hs_cross_row<real, KP, true><<<grid_for(own.R, 4), BLOCK, smem, stream_>>>(
+                  own.R, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.yptr.p, own.ycol.p, h.Q1, QTQ_.p, w_, h_.p, run);
+            else
+              k_hs_cross_row<real, KP, false><<<grid_for(own.R, 4), BLOCK, smem, stream_>>>(
+                  own.R, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.yptr.p, own.ycol.p, h.Q1, QTQ_.p, w_, h_.p, run);
+          });
+        } else {
+          DevSide<real> &other = h.user ? V_ : U_;
+          const double n1 = (double)other.R;
+          const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
+                               (double)own.R * KP * rs * 2;
+          prof_launch("hs_side_row", bytes, [&] {
+            k_hs_side_row<real, KP><<<grid_for(own.R, 4 * Gm::NSG), BLOCK, 0, stream_>>>(
+                own.R, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.yptr.p, h.Q1, w_, n1, h_.p, run);
+          });
+        }
+      }
+      scatter(F, run);
+      const uint64_t nv = h.D * KP / Gm::VE;
+      prof_launch("hv_fin", (double)h.D * KP * rs * 4, [&] {
+        k_hv_fin<real, KP><<<grid_for(nv, BLOCK, 2048), BLOCK, 0, stream_>>>(it, nv, h.fw, lam_, acc_.p, Vd_.p,
+                                                                            Hv_.p, st_.p, part_.p);
+      });
+    });
+  }
+
+  void cg_tail(HalfCtx &h, int it) {
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      using Gm = Geo<real, KP>;
+      const uint64_t nv = h.D * KP / Gm::VE;
+      const double rs = sizeof(real);
+      prof_launch("cg_update", (double)h.D * KP * rs * 6, [&] {
+        k_cg_upd<real, KP><<<grid_for(nv, BLOCK, 2048), BLOCK, 0, stream_>>>(it, nv, Vd_.p, Hv_.p, S_.p, Rv_.p,
+                                                                            st_.p, part_.p, run_host_dev_);
+      });
+      prof_launch("cg_dir", (double)h.D * KP * rs * 3, [&] {
+        k_cg_dir<real, KP><<<grid_for(nv, BLOCK, 2048), BLOCK, 0, stream_>>>(it, nv, Vd_.p, Rv_.p, st_.p);
+      });
+    });
+  }
+
+  // One half of a block: gradient, Newton-CG, update (ffm.cpp:826-832, 843-849).
+  void half(uint32_t f1, uint32_t f2, int which) {
+    HalfCtx h = half_ctx(f1, f2, which);
+    gradient(h);
+    // CG with one iteration of look-ahead (see file header).
+    std::vector<hipEvent_t> evs;
+    int it = 1;
+    for (; it <= MAXCG; it++) {
+      hv_pass(h, it);
+      cg_tail(h, it);
+      hipEvent_t e = ev();
+      HIPCHK(hipEventRecord(e, stream_));
+      evs.push_back(e);
+      if (it >= 2) {
+        HIPCHK(hipEventSynchronize(evs[it - 2]));
+        if (!__atomic_load_n(&run_host_[it], __ATOMIC_ACQUIRE)) break;  // iteration `it` was a no-op
+      }
+    }
+    for (auto e : evs) ev_free_.push_back(e);
+    // apply + update (the last verdict is read after the stream drains below)
+    DevSide<real> &own = *h.own;
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      using Gm = Geo<real, KP>;
+      const double rs = sizeof(real);
+      const uint64_t nv = h.D * KP / Gm::VE;
+      prof_launch("apply_step", (double)h.D * KP * rs * 3, [&] {
+        k_axpy1<real><<<grid_for(nv, BLOCK, 2048), BLOCK, 0, stream_>>>(nv, S_.p, h.W1);
+      });
+      if (own.R == 0) return;
+      DevField<real> &F = *h.F;
+      if (h.cross) {
+        DevSide<real> &other = *h.partner;
+        const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
+                             (double)own.R * KP * rs * 2 + (double)own.npos * (4 + 4 + 4 * rs) +
+                             (double)other.R * KP * rs;
+        prof_launch("update_cross_row", bytes, [&] {
+          k_update_cross_row<real, KP><<<grid_for(own.R, 4), BLOCK, 0, stream_>>>(
+              own.R, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, own.yptr.p, own.ycol.p, own.yt.p, other.yt.p,
+              own.perm.p, h.Q1);
+        });
+      } else {
+        DevSide<real> &other = h.user ? V_ : U_;
+        const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
+                             (double)own.R * KP * rs * 3 + (double)own.R * rs * 2 + (double)own.npos * (4 + 4 * rs);
+        prof_launch("update_side_row", bytes, [&] {
+          k_update_side_row<real, KP><<<grid_for(own.R, 4), BLOCK, 0, stream_>>>(
+              own.R, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, h.Q1, own.bias.p, own.yptr.p, own.yt.p,
+              other.yt.p, own.perm.p);
+        });
+      }
+    });
+    // CG count of this half: the last iteration that ran
+    HIPCHK(hipStreamSynchronize(stream_));
+    int nr = 0;
+    for (int t = 1; t <= MAXCG; t++)
+      if (__atomic_load_n(&run_host_[t], __ATOMIC_ACQUIRE)) nr = t;
+    cg_log.push_back(nr);
+    account_half(h, nr);
+  }
+
+  // Algorithmic bytes of one half (SURVEY §8d formula, s = sizeof(real)).
+  void account_half(const HalfCtx &h, int c) {
+    const double s = sizeof(real), k = (double)kp_;
+    const double R = (double)h.own->R, D = (double)h.D, P = (double)h.own->npos;
+    const double csr = 8 * R + (double)h.F->nnz * (4 + s);
+    if (!h.cross) {
+      const double Rp = (double)(h.user ? V_.R : U_.R);
+      const double gd = P * s + 8 * R + 2 * R * s + Rp * s + R * k * s + csr + 2 * D * k * s;
+      const double hs = c * (8 * R + R * k * s + csr + 9 * D * k * s);
+      const double upd = 4 * D * k * s + csr + 3 * R * k * s + 2 * R * s + 2 * P * s + 8 * R;
+      alg_bytes += gd + hs + upd;
+    } else {
+      const double Rp = (double)h.partner->R, Cc = (double)C_;
+      const double gd = (Cc + 2) * Rp * k * s + Rp * s + Cc * R * k * s + 8 * R + P * (4 + s) + R * s + csr +
+                        2 * D * k * s;
+      const double hs = Rp * k * s + c * (csr + 8 * R + 4 * P + Rp * k * s + 9 * D * k * s);
+      const double upd = 4 * D * k * s + csr + 2 * R * k * s + 2 * P * s + 4 * P + 8 * R + Rp * k * s;
+      alg_bytes += gd + hs + upd;
+    }
+  }
+
+  // ------------------------------------------------------------- state
+  ocffm_param prm_;
+  Comm comm_;
+  bool has_test_;
+  bool inited_ = false;
+  hipStream_t stream_ = nullptr;
+  uint32_t k_, kp_, fu_, fv_, f_, C_ = 0;
+  double w_, lam_, r_;
+  uint64_t m_glob_ = 0, n_ = 0, u0_ = 0, u1_ = 0, dmax_ = 0, npop_ = 0;
+  DevSide<real> U_, V_, T_;
+  std::vector<Block> blocks_;
+  std::vector<DevBuf<real>> W_, H_, P_, Q_;
+  DevBuf<real> acc_, G_, S_, Vd_, Rv_, Hv_, h_, M_, QTQ_;
+  DevBuf<double> sums_, vecs_, part_, at_d_, popular_;
+  DevBuf<uint8_t> cold_;
+  DevBuf<CgState> st_;
+  DevBuf<real *> tabs_;
+  int *run_host_ = nullptr, *run_host_dev_ = nullptr;
+  real *stage_ = nullptr;
+  struct Pending {
+    std::string name;
+    double bytes;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending_;
+  std::vector<hipEvent_t> ev_pool_, ev_free_;
+};
+
+}  // namespace ocffm
+
+// ====================================================================== ABI
+using namespace ocffm;
+
+struct ocffm_data {
+  HostData d;
+};
+struct ocffm_problem {
+  std::unique_ptr<ProblemBase> p;
+};
+
+template <class F> static int guarded(F &&f) {
+  try {
+    f();
+    return OCFFM_OK;
+  } catch (Error &e) {
+    g_last_error = e.what();
+    return e.code;
+  } catch (std::invalid_argument &e) {
+    g_last_error = std::string("invalid argument: ") + e.what();
+    return OCFFM_E_ARG;
+  } catch (std::out_of_range &e) {
+    g_last_error = std::string("out of range: ") + e.what();
+    return OCFFM_E_DATA;
+  } catch (std::bad_alloc &) {
+    g_last_error = "host out of memory";
+    return OCFFM_E_HIP;
+  } catch (std::exception &e) {
+    g_last_error = e.what();
+    return OCFFM_E_IO;
+  }
+}
+
+extern "C" {
+
+void ocffm_param_default(ocffm_param *p) {
+  p->omega = 0.1;
+  p->lambda = 1e-5;
+  p->r = -1;
+  p->nr_pass = 20;
+  p->k = 4;
+  p->nr_threads = 1;
+  p->self_side = 1;
+  p->freq = 0;
+  p->precision = OCFFM_FP64;
+  p->device = 0;
+}
+
+const char *ocffm_last_error(void) { return g_last_error.c_str(); }
+
+int ocffm_device_count(int *count) {
+  return guarded([&] {
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    *count = e == hipSuccess ? c : 0;
+  });
+}
+
+int ocffm_data_read(const char *path, int has_label, const uint64_t *ds, uint32_t nds, ocffm_data **out) {
+  return guarded([&] {
+    auto d = std::make_unique<ocffm_data>();
+    Rows r = parse_rows(path, has_label != 0, ds, nds);
+    build(d->d, r);
+    d->d.path = path;
+    *out = d.release();
+  });
+}
+
+int ocffm_data_from_rows(uint64_t m, const uint64_t *xptr, const uint32_t *fid, const uint64_t *idx,
+                         const double *val, const uint64_t *yptr, const uint64_t *ycol, const uint64_t *ds,
+                         uint32_t nds, ocffm_data **out) {
+  return guarded([&] {
+    Rows r;
+    r.has_label = yptr != nullptr;
+    for (uint64_t i = 0; i < m; i++) {
+      for (uint64_t p = xptr[i]; p < xptr[i + 1]; p++) {
+        r.f = std::max<uint64_t>(r.f, (uint64_t)fid[p] + 1);
+        if (ds != nullptr && (fid[p] >= nds || ds[fid[p]] <= idx[p])) continue;
+        r.fid.push_back(fid[p]);
+        r.idx.push_back(idx[p]);
+        r.val.push_back(val[p]);
+      }
+      r.xptr.push_back(r.fid.size());
+      if (r.has_label) {
+        for (uint64_t p = yptr[i]; p < yptr[i + 1]; p++) {
+          r.ycol.push_back(ycol[p]);
+          r.n = std::max<uint64_t>(r.n, ycol[p] + 1);
+        }
+        r.yptr.push_back(r.ycol.size());
+      }
+    }
+    auto d = std::make_unique<ocffm_data>();
+    build(d->d, r);
+    *out = d.release();
+  });
+}
+
+int ocffm_data_trans_y(ocffm_data *V, const ocffm_data *U) {
+  return guarded([&] { trans_y(V->d, U->d); });
+}
+
+int ocffm_data_get_info(const ocffm_data *d, ocffm_data_info *o) {
+  return guarded([&] {
+    o->m = d->d.m;
+    o->n = d->d.n;
+    o->f = d->d.f;
+    uint64_t nx = 0;
+    for (auto &v : d->d.xidx) nx += v.size();
+    o->nnz_x = nx;
+    o->nnz_y = d->d.ycol.size();
+  });
+}
+
+int ocffm_data_get_ds(const ocffm_data *d, uint64_t *out) {
+  return guarded([&] {
+    for (size_t i = 0; i < d->d.Ds.size(); i++) out[i] = d->d.Ds[i];
+  });
+}
+
+void ocffm_data_free(ocffm_data *d) { delete d; }
+
+static int create_impl(const ocffm_data *U, const ocffm_data *Ut, const ocffm_data *V, const ocffm_param *p,
+                       Comm comm, ocffm_problem **out) {
+  return guarded([&] {
+    if (!U || !V || !p || !out) throw Error(OCFFM_E_ARG, "null argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+      throw Error(OCFFM_E_HIP, "no HIP device visible (this build has no CPU fallback)");
+    auto pr = std::make_unique<ocffm_problem>();
+    const HostData *ut = Ut ? &Ut->d : nullptr;
+    if (p->precision == OCFFM_FP32)
+      pr->p = std::make_unique<Problem<float>>(U->d, ut, V->d, *p, comm);
+    else if (p->precision == OCFFM_FP64)
+      pr->p = std::make_unique<Problem<double>>(U->d, ut, V->d, *p, comm);
+    else
+      throw Error(OCFFM_E_ARG, "precision must be 32 or 64");
+    *out = pr.release();
+  });
+}
+
+int ocffm_problem_create(const ocffm_data *U, const ocffm_data *Ut, const ocffm_data *V, const ocffm_param *p,
+                         ocffm_problem **out) {
+  return create_impl(U, Ut, V, p, Comm{}, out);
+}
+
+int ocffm_comm_id(void *out) {
+  return guarded([&] {
+    static_assert(sizeof(ncclUniqueId) <= OCFFM_COMM_ID_BYTES, "id size");
+    ncclUniqueId id;
+    NCCLCHK(ncclGetUniqueId(&id));
+    std::memset(out, 0, OCFFM_COMM_ID_BYTES);
+    std::memcpy(out, &id, sizeof(id));
+  });
+}
+
+int ocffm_problem_create_dist(const ocffm_data *U, const ocffm_data *Ut, const ocffm_data *V, const ocffm_param *p,
+                              int rank, int nranks, const void *comm_id, ocffm_problem **out) {
+  Comm c;
+  int st = guarded([&] {
+    if (nranks < 1 || rank < 0 || rank >= nranks) throw Error(OCFFM_E_ARG, "bad rank/nranks");
+    c.rank = rank;
+    c.nranks = nranks;
+    if (nranks > 1) {
+      HIPCHK(hipSetDevice(p->device));
+      ncclUniqueId id;
+      std::memcpy(&id, comm_id, sizeof(id));
+      NCCLCHK(ncclCommInitRank(&c.nccl, nranks, id, rank));
+    }
+  });
+  if (st != OCFFM_OK) return st;
+  st = create_impl(U, Ut, V, p, c, out);
+  if (st != OCFFM_OK && c.nccl) ncclCommDestroy(c.nccl);
+  return st;
+}
+
+int ocffm_problem_create_dist_host(const ocffm_data *U, const ocffm_data *Ut, const ocffm_data *V,
+                                   const ocffm_param *p, int rank, int nranks, ocffm_allreduce_fn fn, void *user,
+                                   ocffm_problem **out) {
+  Comm c;
+  c.rank = rank;
+  c.nranks = nranks;
+  c.host_fn = fn;
+  c.host_user = user;
+  if (nranks < 1 || rank < 0 || rank >= nranks || !fn) {
+    g_last_error = "bad rank/nranks/callback";
+    return OCFFM_E_ARG;
+  }
+  return create_impl(U, Ut, V, p, c, out);
+}
+
+#define PROB_CALL(body)                                    \
+  return guarded([&] {                                     \
+    if (!prob || !prob->p) throw Error(OCFFM_E_ARG, "null problem"); \
+    body;                                                  \
+  })
+
+int ocffm_problem_init(ocffm_problem *prob) { PROB_CALL(prob->p->init()); }
+int ocffm_problem_one_epoch(ocffm_problem *prob) { PROB_CALL(prob->p->one_epoch()); }
+int ocffm_problem_solve_block(ocffm_problem *prob, uint32_t f1, uint32_t f2) {
+  PROB_CALL(prob->p->solve_block(f1, f2));
+}
+int ocffm_problem_cache_sasb(ocffm_problem *prob) { PROB_CALL(prob->p->cache_sasb()); }
+int ocffm_problem_validate(ocffm_problem *prob, ocffm_metrics *m) { PROB_CALL(prob->p->validate(m)); }
+
+int ocffm_print_header(void) {
+  std::cout << "iter";
+  uint32_t s = 5;
+  for (int i = 0; i < 5; i++, s *= 2) {
+    std::cout.width(9);
+    std::cout << "( p@ " << s << ", ";
+    std::cout.width(6);
+    std::cout << "nDCG@" << s << " )";
+  }
+  std::cout.width(12);
+  std::cout << "ploss" << std::endl;
+  return OCFFM_OK;
+}
+
+int ocffm_print_epoch(const ocffm_metrics *m, uint32_t t) {
+  std::cout.width(2);
+  std::cout << t + 1;
+  if (m) {
+    for (int i = 0; i < 5; i++) {
+      std::cout.width(9);
+      std::cout << "( " << std::setprecision(3) << m->prec[i] * 100 << " ,";
+      std::cout.width(6);
+      std::cout << std::setprecision(3) << m->ndcg[i] * 100 << " )";
+    }
+    std::cout.width(13);
+    std::cout << std::setprecision(3) << m->loss;
+  }
+  std::cout << std::endl;
+  return OCFFM_OK;
+}
+
+// ffm.cpp:1147-1161.
+int ocffm_problem_solve(ocffm_problem *prob) {
+  PROB_CALL({
+    ProblemBase &P = *prob->p;
+    const bool talk = P.rank() == 0;
+    if (P.has_test() && talk) ocffm_print_header();
+    for (uint32_t it = 0; it < P.nr_pass(); it++) {
+      P.one_epoch();
+      if (P.has_test() && it % 10 == 9) {
+        ocffm_metrics m;
+        P.validate(&m);
+        if (talk) ocffm_print_epoch(&m, it);
+      }
+    }
+  });
+}
+
+int ocffm_problem_get(ocffm_problem *prob, char what, uint32_t b12, double *out, uint64_t cap, uint64_t *len) {
+  PROB_CALL({
+    uint64_t n = prob->p->get(what, b12, out, cap);
+    if (len) *len = n;
+  });
+}
+int ocffm_problem_set(ocffm_problem *prob, char what, uint32_t b12, const double *in, uint64_t len) {
+  PROB_CALL(prob->p->set(what, b12, in, len));
+}
+int ocffm_problem_grad(ocffm_problem *prob, uint32_t f1, uint32_t f2, int half, double *out) {
+  PROB_CALL(prob->p->grad(f1, f2, half, out));
+}
+int ocffm_problem_hv(ocffm_problem *prob, uint32_t f1, uint32_t f2, int half, const double *v, double *out) {
+  PROB_CALL(prob->p->hv(f1, f2, half, v, out));
+}
+int ocffm_problem_save_model(ocffm_problem *prob, const char *path) { PROB_CALL(prob->p->save_model(path)); }
+
+int ocffm_problem_cg_log(ocffm_problem *prob, int32_t *out, int cap, int *count) {
+  PROB_CALL({
+    auto &l = prob->p->cg_log;
+    for (int i = 0; i < (int)l.size() && i < cap; i++) out[i] = l[i];
+    if (count) *count = (int)l.size();
+  });
+}
+int ocffm_problem_set_profiling(ocffm_problem *prob, int on) { PROB_CALL(prob->p->profiling = on != 0); }
+int ocffm_problem_set_profile_filter(ocffm_problem *prob, const char *name) {
+  PROB_CALL(prob->p->prof_filter = name ? name : "");
+}
+int ocffm_problem_kernel_stats(ocffm_problem *prob, ocffm_kernel_stat *out, int cap, int *count) {
+  PROB_CALL({
+    int i = 0;
+    for (auto &kv : prob->p->kstats) {
+      if (i < cap && out) {
+        std::memset(&out[i], 0, sizeof(ocffm_kernel_stat));
+        std::strncpy(out[i].name, kv.first.c_str(), sizeof(out[i].name) - 1);
+        out[i].launches = kv.second.launches;
+        out[i].total_ms = kv.second.ms;
+        out[i].alg_bytes = kv.second.bytes;
+      }
+      i++;
+    }
+    if (count) *count = i;
+  });
+}
+int ocffm_problem_reset_stats(ocffm_problem *prob) {
+  PROB_CALL({
+    prob->p->kstats.clear();
+    prob->p->cg_log.clear();
+    prob->p->alg_bytes = 0;
+  });
+}
+int ocffm_problem_alg_bytes(ocffm_problem *prob, double *bytes) { PROB_CALL(*bytes = prob->p->alg_bytes); }
+int ocffm_problem_sync(ocffm_problem *prob) { PROB_CALL(prob->p->sync()); }
+void ocffm_problem_destroy(ocffm_problem *prob) { delete prob; }
+
+}  // extern "C"

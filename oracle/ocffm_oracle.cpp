@@ -1097,6 +1097,25 @@ void orc_set(void *c, char what, uint32_t b12, const double *in, uint64_t len) {
   dst->assign(in, in + len);
 }
 
+// Recompute every derived quantity (P, Q, a, b, sa, sb, y~) from W and H,
+// as init() does after drawing them: lets tests perturb W/H and evaluate
+// func() (finite-difference checks of gd_*/hs_*).
+void orc_refresh(void *c) {
+  Problem &p = ((OrcCtx *)c)->prob;
+  for (u32 f1 = 0; f1 < p.f; f1++)
+    for (u32 f2 = f1; f2 < p.f; f2++) {
+      if (!p.block_used(f1, f2)) continue;
+      const u32 b12 = block_index(f1, f2, p.f);
+      p.utx(p.is_user(f1) ? *p.U : *p.V, p.is_user(f1) ? f1 : f1 - p.fu, p.W[b12], p.P[b12]);
+      p.utx(p.is_user(f2) ? *p.U : *p.V, p.is_user(f2) ? f2 : f2 - p.fu, p.H[b12], p.Q[b12]);
+    }
+  std::fill(p.a.begin(), p.a.end(), 0.0);
+  std::fill(p.b.begin(), p.b.end(), 0.0);
+  p.cache_sasb();
+  if (p.prm.self_side) p.calc_side();
+  p.init_y_tilde();
+}
+
 // Gradient of one half without changing state: half 0 = W of block (f1,f2)
 // (rows of f1's side), half 1 = H (rows of f2's side).
 void orc_grad(void *c, uint32_t f1, uint32_t f2, int half, double *G) {

@@ -44,7 +44,7 @@ def lib():
         L.orc_problem_new.restype = C.c_void_p
         L.orc_problem_new.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_double, C.c_double, C.c_double,
                                       C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_int]
-        for name in ("orc_problem_free", "orc_init", "orc_one_epoch", "orc_cache_sasb"):
+        for name in ("orc_problem_free", "orc_init", "orc_one_epoch", "orc_cache_sasb", "orc_refresh"):
             getattr(L, name).argtypes = [C.c_void_p]
         L.orc_srand.argtypes = [C.c_uint32]
         L.orc_solve_block.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
@@ -61,6 +61,7 @@ def lib():
         L.orc_grad.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, _f64p]
         L.orc_hv.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, _f64p, _f64p]
         L.orc_save_model.argtypes = [C.c_void_p, C.c_char_p]
+        L.orc_times.argtypes = [C.c_void_p, C.c_int]
         L.orc_time_epochs.restype = C.c_double
         L.orc_time_epochs.argtypes = [C.c_void_p, C.c_uint32]
         _lib = L
@@ -137,6 +138,9 @@ class Oracle:
 
     def one_epoch(self):
         lib().orc_one_epoch(self.h)
+
+    def refresh(self):
+        lib().orc_refresh(self.h)
 
     def solve_block(self, f1, f2):
         lib().orc_solve_block(self.h, f1, f2)

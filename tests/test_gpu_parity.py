@@ -1,0 +1,220 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Tolerances (written here):
+  fp64 mode  : state (W, H, P, Q, a, b, y~) and objective within 1e-9 relative
+               of the oracle; CG iteration counts identical; p@k / nDCG@k
+               identical up to 1e-12.
+  fp32 mode  : objective and ploss within 1e-3 relative, p@k and nDCG@k
+               within 2e-2 absolute (SURVEY §8c measured fp32 drift).
+Init is bit-exact in both modes' source tables: W/H come from the same host
+rand() stream as the reference (ffm.cpp:71-78).
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import ocffm
+import oracle_lib as O
+import synth
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TRAIN = os.path.join(REPO, "one-class-ffm_amd", "train")
+ORACLE_TRAIN = os.path.join(REPO, "oracle", "oracle_train")
+
+
+def pair(ds, precision=ocffm.FP64, self_side=True, freq=False, with_test=True, **kw):
+    o = O.Oracle(ds, self_side=self_side, freq=freq, with_test=with_test, **kw)
+    g = ocffm.problem_from_dataset(ds, precision=precision, self_side=self_side, freq=freq, with_test=with_test,
+                                   **kw)
+    ocffm.srand(1)
+    o.init()
+    ocffm.srand(1)
+    g.init()
+    return o, g
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(1e-300, np.abs(b).max())) if b.size else 0.0
+
+
+def state_names(o):
+    out = []
+    for f1 in range(o.f):
+        for f2 in range(f1, o.f):
+            if not o.self_side and not (f1 < o.fu <= f2):
+                continue
+            out.append(O.block_index(f1, f2, o.f))
+    return out
+
+
+def assert_state(o, g, tol, check_yt=True):
+    for b12 in state_names(o):
+        for what in "WHPQ":
+            assert rel(g.get(what, b12), o.get(what, b12)) <= tol, (what, b12)
+    for what in "ab":
+        assert rel(g.get(what), o.get(what)) <= tol, what
+    if check_yt:
+        assert rel(g.get("u"), o.get("u")) <= tol
+        assert rel(g.get("v"), o.get("v")) <= tol
+
+
+def gpu_objective(o, g):
+    """Objective of the GPU state: load its W/H into the oracle and evaluate
+    the reference's func() (ffm.cpp:1321-1351)."""
+    for b12 in state_names(o):
+        o.set("W", b12, g.get("W", b12))
+        o.set("H", b12, g.get("H", b12))
+    o.refresh()
+    return o.func()
+
+
+def test_init_state(tiny):
+    o, g = pair(tiny)
+    for b12 in state_names(o):
+        np.testing.assert_array_equal(g.get("W", b12), o.get("W", b12))  # same host stream
+        np.testing.assert_array_equal(g.get("H", b12), o.get("H", b12))
+    assert_state(o, g, 1e-13)
+    assert rel(g.get("s"), o.get("s")) <= 1e-12
+    assert rel(g.get("t"), o.get("t")) <= 1e-12
+
+
+@pytest.mark.parametrize("self_side", [True, False])
+def test_gradient_and_hv_kernels(self_side):
+    ds = synth.general(seed=5, m=60, n=40, fu=2, fv=2, k=5, nnz_user=2, mean_pos=3.0, vals="real")
+    o, g = pair(ds, self_side=self_side, with_test=False)
+    rng = np.random.default_rng(0)
+    for f1 in range(o.f):
+        for f2 in range(f1, o.f):
+            if not self_side and not (f1 < o.fu <= f2):
+                continue
+            for half in (0, 1):
+                G0, G1 = o.grad(f1, f2, half), g.grad(f1, f2, half)
+                assert rel(G1, G0) <= 1e-12, ("grad", f1, f2, half)
+                v = rng.standard_normal(G0.size)
+                H0, H1 = o.hv(f1, f2, half, v), g.hv(f1, f2, half, v)
+                assert rel(H1, H0) <= 1e-12, ("hv", f1, f2, half)
+
+
+def test_block_by_block_fp64(tiny):
+    o, g = pair(tiny)
+    for f1 in range(o.f):
+        for f2 in range(f1, o.f):
+            o.solve_block(f1, f2)
+            g.solve_block(f1, f2)
+            assert_state(o, g, 1e-9)
+    np.testing.assert_array_equal(g.cg_log(), o.cg_log())
+
+
+def test_epochs_fp64_tiny(tiny):
+    o, g = pair(tiny)
+    for e in range(3):
+        o.one_epoch()
+        g.one_epoch()
+        assert_state(o, g, 1e-9)
+        assert rel(g.get("s"), o.get("s")) <= 1e-9
+        vo, vg = o.validate(), g.validate()
+        assert abs(vg["loss"] - vo["loss"]) <= 1e-9 * abs(vo["loss"])
+        np.testing.assert_allclose(vg["prec"], vo["prec"], atol=1e-12)
+        np.testing.assert_allclose(vg["ndcg"], vo["ndcg"], atol=1e-12)
+    np.testing.assert_array_equal(g.cg_log(), o.cg_log())
+
+
+def test_epochs_fp32_tiny(tiny):
+    o, g = pair(tiny, precision=ocffm.FP32)
+    for e in range(3):
+        o.one_epoch()
+        g.one_epoch()
+    vo, vg = o.validate(), g.validate()
+    assert abs(vg["loss"] - vo["loss"]) <= 1e-3 * abs(vo["loss"])
+    np.testing.assert_allclose(vg["prec"], vo["prec"], atol=2e-2)
+    np.testing.assert_allclose(vg["ndcg"], vo["ndcg"], atol=2e-2)
+    # objective of the fp32 state, evaluated in fp64 by a second oracle
+    f_ref = o.func()
+    o2 = O.Oracle(tiny)
+    ocffm.srand(1)
+    o2.init()
+    f32obj = gpu_objective(o2, g)
+    assert abs(f32obj - f_ref) <= 1e-3 * abs(f_ref)
+
+
+@pytest.mark.parametrize("variant", ["ns", "freq", "k5", "k16", "multi_nnz"])
+def test_variants_fp64(variant):
+    kw = {}
+    if variant == "multi_nnz":
+        ds = synth.general(seed=9, m=150, n=70, fu=3, fv=2, k=8, nnz_user=3, mean_pos=4.0, vals="real", test_rows=30)
+    else:
+        ds = synth.tiny(seed=4)
+    if variant == "k5":
+        kw["k"] = 5
+    if variant == "k16":
+        kw["k"] = 16
+    o, g = pair(ds, self_side=variant != "ns", freq=variant == "freq", **kw)
+    for e in range(2):
+        o.one_epoch()
+        g.one_epoch()
+    assert_state(o, g, 1e-9)
+    np.testing.assert_array_equal(g.cg_log(), o.cg_log())
+    vo, vg = o.validate(), g.validate()
+    assert abs(vg["loss"] - vo["loss"]) <= 1e-9 * abs(vo["loss"])
+    np.testing.assert_allclose(vg["ndcg"], vo["ndcg"], atol=1e-12)
+
+
+def test_kkbox_small_fp64(kk_small):
+    o, g = pair(kk_small)
+    o.one_epoch()
+    g.one_epoch()
+    assert_state(o, g, 1e-9)
+    np.testing.assert_array_equal(g.cg_log(), o.cg_log())
+    vo, vg = o.validate(), g.validate()
+    np.testing.assert_allclose(vg["prec"], vo["prec"], atol=1e-12)
+
+
+def test_cold_rows_and_duplicate_labels():
+    ds = synth.tiny(seed=6)
+    # a test row whose features are all dropped -> popularity scores
+    t = ds.test
+    t.idx[0] = 10_000
+    t.idx[1] = 10_000
+    o, g = pair(ds)
+    o.one_epoch()
+    g.one_epoch()
+    vo, vg = o.validate(), g.validate()
+    assert abs(vg["loss"] - vo["loss"]) <= 1e-9 * abs(vo["loss"])
+    np.testing.assert_allclose(vg["prec"], vo["prec"], atol=1e-12)
+
+
+def test_cli_matches_oracle_cli(tiny, tmp_path):
+    paths = tiny.write(str(tmp_path))
+    args = ["-k", "4", "-t", "10", "-p", paths["test"], "-o"]
+    r1 = subprocess.run([TRAIN] + args + [str(tmp_path / "gpu.model"), paths["item"], paths["train"]],
+                        capture_output=True, text=True, timeout=300)
+    r2 = subprocess.run([ORACLE_TRAIN] + args + [str(tmp_path / "cpu.model"), paths["item"], paths["train"]],
+                        capture_output=True, text=True, timeout=300)
+    assert r1.returncode == 0, r1.stderr
+    assert r2.returncode == 0, r2.stderr
+    assert r1.stdout == r2.stdout
+    a = open(tmp_path / "gpu.model").read().split("\n")
+    b = open(tmp_path / "cpu.model").read().split("\n")
+    assert len(a) == len(b)
+    diff = sum(x != y for x, y in zip(a, b))
+    assert diff <= len(a) // 100  # 6-significant-digit text; rounding-boundary lines only
+
+
+def test_kkbox_full_size_properties():
+    """Config-3 size: size-independent properties after one fp32 epoch."""
+    ds = synth.kkbox()
+    g = ocffm.problem_from_dataset(ds, precision=ocffm.FP32, with_test=False)
+    ocffm.srand(1)
+    g.init()
+    g.one_epoch()
+    cg = g.cg_log()
+    assert cg.size == 30 and cg.min() >= 1 and cg.max() <= 20
+    yu, yv = g.get("u"), g.get("v")
+    assert np.isfinite(yu).all()
+    # both orientations of y~ hold identical values (ffm.cpp:455,462)
+    assert np.array_equal(np.sort(yu), np.sort(yv))

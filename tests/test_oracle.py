@@ -1,0 +1,134 @@
+"""CPU tests of the oracle itself: pin it before trusting it.
+
+1. The reference's only known-answer test (script/nDCG_degub_tool): with the
+   scores forced to z_j = n - j, nDCG@10 per row must equal gen_ans.py's
+   output (tests/golden/ndcg_kat/expected_ndcg10.txt, 4 d.p.).
+2. Math identities against the reference's own objective func()
+   (ffm.cpp:1321-1351): the restated gradients (gd_side / gd_cross,
+   ffm.cpp:537-703) equal finite differences of func, and the restated
+   Hessian-vector products (hs_side / hs_cross + lambda*v, ffm.cpp:594-742)
+   equal second differences (func is exactly quadratic in one table).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import synth
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "ndcg_kat")
+
+
+def test_ndcg_known_answer():
+    import ctypes as C
+    L = O.lib()
+    U = O.data_read(os.path.join(GOLD, "case1.mf"), True)
+    V = O.data_read(os.path.join(GOLD, "test_item.mf"), False)
+    Ut = O.data_read(os.path.join(GOLD, "case1.mf"), True, O.data_ds(U))
+    # readme:10 runs `train -k 8 -t 1 -p case1.mf test_item.mf case1.mf`
+    h = L.orc_problem_new(U, Ut, V, 0.1, 1e-5, -1.0, 1, 8, 1, 1, 0)
+    L.orc_srand(1)
+    L.orc_init(h)
+    out = np.zeros(11)
+    rows = np.zeros(20)
+    L.orc_validate(h, 1, out, rows.ctypes.data_as(C.c_void_p))
+    L.orc_problem_free(h)
+    expected = np.loadtxt(os.path.join(GOLD, "expected_ndcg10.txt"))
+    assert expected.shape == (20,)
+    np.testing.assert_array_equal(np.round(rows, 4), expected)
+
+
+def _small(self_side=True):
+    ds = synth.general(seed=3, m=12, n=9, fu=2, fv=2, k=3, d_user=[5, 4], d_item=[6, 3], nnz_user=2,
+                       mean_pos=2.0, vals="real")
+    o = O.Oracle(ds, k=3, omega=0.3, lam=0.7, r=-0.5, self_side=self_side, with_test=False)
+    O.lib().orc_srand(1)
+    o.init()
+    return o
+
+
+@pytest.mark.parametrize("self_side", [True, False])
+def test_gradient_is_derivative_of_objective(self_side):
+    o = _small(self_side)
+    f = o.f
+    eps = 1e-6
+    rng = np.random.default_rng(0)
+    for f1 in range(f):
+        for f2 in range(f1, f):
+            if not self_side and not (f1 < o.fu <= f2):
+                continue
+            b12 = O.block_index(f1, f2, f)
+            for half, what in ((0, "W"), (1, "H")):
+                G = o.grad(f1, f2, half)
+                base = o.get(what, b12)
+                for idx in rng.choice(base.size, size=min(6, base.size), replace=False):
+                    t = base.copy()
+                    t[idx] += eps
+                    o.set(what, b12, t)
+                    o.refresh()
+                    fp = o.func()
+                    t[idx] -= 2 * eps
+                    o.set(what, b12, t)
+                    o.refresh()
+                    fm = o.func()
+                    o.set(what, b12, base)
+                    o.refresh()
+                    fd = (fp - fm) / (2 * eps)
+                    assert abs(fd - G[idx]) <= 1e-5 * max(1.0, abs(G[idx])), (f1, f2, half, idx, fd, G[idx])
+
+
+@pytest.mark.parametrize("self_side", [True, False])
+def test_hessian_vector_is_second_derivative(self_side):
+    o = _small(self_side)
+    f = o.f
+    rng = np.random.default_rng(1)
+    for f1 in range(f):
+        for f2 in range(f1, f):
+            if not self_side and not (f1 < o.fu <= f2):
+                continue
+            b12 = O.block_index(f1, f2, f)
+            for half, what in ((0, "W"), (1, "H")):
+                base = o.get(what, b12)
+                v = rng.standard_normal(base.size)
+                hv = o.hv(f1, f2, half, v)
+                eps = 1e-3
+                vals = []
+                for s in (1, -1, 0):
+                    o.set(what, b12, base + s * eps * v)
+                    o.refresh()
+                    vals.append(o.func())
+                o.set(what, b12, base)
+                o.refresh()
+                fd = (vals[0] + vals[1] - 2 * vals[2]) / eps ** 2
+                vhv = float(v @ hv)
+                assert abs(fd - vhv) <= 1e-4 * max(1.0, abs(vhv)), (f1, f2, half, fd, vhv)
+
+
+def test_epochs_decrease_objective(tiny):
+    o = O.Oracle(tiny, with_test=True)
+    O.lib().orc_srand(1)
+    o.init()
+    prev = o.func()
+    for _ in range(3):
+        o.one_epoch()
+        cur = o.func()
+        assert cur < prev
+        prev = cur
+    cg = o.cg_log()
+    assert cg.size == 3 * 2 * 6 and cg.min() >= 1 and cg.max() <= 20
+
+
+def test_init_stream_matches_documented_bound(tiny):
+    """W/H ~ U(-b, b), b = 0.1*qrsqrt(k) (ffm.cpp:71-78); qrsqrt(4) != 0.5."""
+    o = O.Oracle(tiny)
+    O.lib().orc_srand(1)
+    o.init()
+    w = o.get("W", 0)
+    x = 4.0
+    i = np.frombuffer(np.float64(x).tobytes(), dtype=np.uint64)[0]
+    i = np.uint64(0x5fe6eb50c7b537a9) - (i >> np.uint64(1))
+    y = np.frombuffer(np.uint64(i).tobytes(), dtype=np.float64)[0]
+    y = y * (1.5 - 0.5 * x * y * y)
+    assert np.abs(w).max() <= 0.1 * y
+    assert np.abs(w).max() > 0.09 * y

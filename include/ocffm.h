@@ -121,8 +121,10 @@ int ocffm_problem_create_dist_host(const ocffm_data *U, const ocffm_data *Ut, co
                                    void *user, ocffm_problem **out);
 
 /* ImpProblem::init (ffm.cpp:467-512).  W/H are drawn on the host from the
- * C library rand() stream exactly as the reference does (ffm.cpp:71-78);
- * call srand() first to change the seed (the reference never does: seed 1). */
+ * C library rand() stream exactly as the reference does (ffm.cpp:71-78).
+ * The reference's init is the first rand() consumer of its process (implicit
+ * seed 1); HIP runtime start-up in ocffm_problem_create may draw from the
+ * stream, so call srand(1) right before this for reference-identical W/H. */
 int ocffm_problem_init(ocffm_problem *p);
 
 /* ImpProblem::one_epoch (ffm.cpp:852-870). */

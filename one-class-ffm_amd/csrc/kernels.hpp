@@ -51,7 +51,18 @@ constexpr double CG_EPS = 9e-2;  // ffm.cpp:762
 
 struct Chunk {  // a run of CSC entries of one feature column
   uint32_t col;
-  uint32_t single;  // 1: the column has exactly this chunk -> plain store
+  uint32_t nch;  // chunks of this column (1: this chunk owns the column)
+  int64_t b, e;
+};
+
+// A run of one row's positives [b, e): rows with many positives (popular
+// items: the Pareto head holds ~all users) are split so that no wave walks
+// tens of thousands of positives alone.  `first` marks the segment that also
+// carries the row-local terms.  Row kernels write one partial per segment;
+// the CSC pass sums a row's segments in order (deterministic, no atomics).
+struct Seg {
+  uint32_t row;
+  uint32_t first;
   int64_t b, e;
 };
 
@@ -127,8 +138,11 @@ __device__ __forceinline__ double block_sum(double v) {
   return t;
 }
 
-// Cross-block reduction by the last-arriving block (MI355X guide G16:
-// release fence + asm vmcnt(0) before the ticket, acquire fence after).
+// Cross-block reduction by the last-arriving block.  Hand-off per the
+// MI355X guide's measured-valid form: partials written with agent-scope
+// (sc1) stores, the writing wave drains vmcnt, one agent-scope atomic add per
+// block; the block whose add returns gridDim-1 reads every partial with sc1
+// loads after a workgroup barrier.  No L2 write-back fence is needed.
 // Partials are summed in block order: deterministic for a fixed grid.
 template <int NV>
 __device__ __forceinline__ bool last_block(const double (&v)[NV], double *part, unsigned *counter,
@@ -136,25 +150,22 @@ __device__ __forceinline__ bool last_block(const double (&v)[NV], double *part, 
   __shared__ int s_last;
   if (threadIdx.x == 0) {
 #pragma unroll
-    for (int k = 0; k < NV; k++) part[(size_t)blockIdx.x * NV + k] = v[k];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    for (int k = 0; k < NV; k++)
+      __hip_atomic_store(&part[(size_t)blockIdx.x * NV + k], v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = atomicAdd(counter, 1u);
+    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = (t == gridDim.x - 1);
-    if (s_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
   }
   __syncthreads();
   if (!s_last) return false;
 #pragma unroll
   for (int k = 0; k < NV; k++) {
     double x = 0;
-    for (unsigned b = threadIdx.x; b < gridDim.x; b += BLOCK) x += __hip_atomic_load(&part[(size_t)b * NV + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += BLOCK)
+      x += __hip_atomic_load(&part[(size_t)b * NV + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     tot[k] = block_sum(x);
   }
-  if (threadIdx.x == 0) *counter = 0u;
+  if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
 }
 
@@ -164,6 +175,16 @@ __device__ __forceinline__ bool last_block(const double (&v)[NV], double *part, 
   const uint64_t nwaves = ((uint64_t)gridDim.x * BLOCK) >> 6;                       \
   (void)lane;                                                                       \
   (void)nwaves;
+
+// CG direction of iteration `it` at feature row d: p_1 = r_0 is stored by
+// the gradient pass; for it > 1 the direction p_it = r + beta p (ffm.cpp:
+// 810-811) is formed on the fly by every reader and stored by the feature
+// pass of iteration it (which owns row d), so no separate direction kernel.
+template <typename real, int KP>
+__device__ __forceinline__ vec_t<real> cg_dir_at(const real *__restrict__ P, const real *__restrict__ Rv, real beta,
+                                                 bool upd, size_t off) {
+  return upd ? vld<real>(Rv + off) + vsplat<real>(beta) * vld<real>(P + off) : vld<real>(P + off);
+}
 
 // ------------------------------------------------------------------ UTX ---
 // out_i = sum_{x in X_i} val * A[idx]  (ffm.cpp:314-331).  One row per subgroup.
@@ -245,11 +266,12 @@ __global__ __launch_bounds__(BLOCK) void k_init_ytilde(uint64_t R, const int64_t
 }
 
 // --------------------------------------------------------- gradient rows ---
-// h_i = pk_i + w (T_i + (a_i - r) oQ + bQ),
-// pk_i = sum_{j in pos(i)} ((1-w) y~_ij - w (1-r)) q_j,  T_i = sum_c P_c[i] M_c
+// Per segment s of row i:
+//   h[s] = sum_{j in seg} ((1-w) y~_ij - w (1-r)) q_j
+//          + [first] w (T_i + (a_i - r) oQ + bQ),   T_i = sum_c P_c[i] M_c
 // (gd_cross row body, ffm.cpp:658-700).  M (C x KP x KP) staged in LDS.
 template <typename real, int KP, bool MLDS>
-__global__ __launch_bounds__(BLOCK) void k_gd_cross_row(uint64_t R, const int64_t *__restrict__ yptr,
+__global__ __launch_bounds__(BLOCK) void k_gd_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                         const uint32_t *__restrict__ ycol,
                                                         const real *__restrict__ yt, const real *__restrict__ Q1,
                                                         int C, const real *const *__restrict__ Ptabs,
@@ -275,11 +297,12 @@ __global__ __launch_bounds__(BLOCK) void k_gd_cross_row(uint64_t R, const int64_
     oQ[e] = (real)sums[li * G::VE + e];
     bQ[e] = (real)sums[KP + li * G::VE + e];
   }
-  for (uint64_t i = wave; i < R; i += nwaves) {
+  for (uint64_t s = wave; s < nseg; s += nwaves) {
+    const Seg sgm = segs[s];
+    const uint64_t i = sgm.row;
     vec_t<real> pk = vzero<real>();
-    int64_t p = yptr[i] + sg;
-    const int64_t pe = yptr[i + 1];
-    for (; p + G::NSG < pe; p += 2 * G::NSG) {
+    int64_t p = sgm.b + sg;
+    for (; p + G::NSG < sgm.e; p += 2 * G::NSG) {
       const uint32_t j0 = ycol[p], j1 = ycol[p + G::NSG];
       const real s0 = cpos * yt[p] - cneg, s1 = cpos * yt[p + G::NSG] - cneg;
       const vec_t<real> q0 = vld<real>(Q1 + (size_t)j0 * KP + li * G::VE);
@@ -287,25 +310,27 @@ __global__ __launch_bounds__(BLOCK) void k_gd_cross_row(uint64_t R, const int64_
       pk += vsplat<real>(s0) * q0;
       pk += vsplat<real>(s1) * q1;
     }
-    if (p < pe) pk += vsplat<real>(cpos * yt[p] - cneg) * vld<real>(Q1 + (size_t)ycol[p] * KP + li * G::VE);
+    if (p < sgm.e) pk += vsplat<real>(cpos * yt[p] - cneg) * vld<real>(Q1 + (size_t)ycol[p] * KP + li * G::VE);
     pk = xsg_vsum<G::LPR, real>(pk);
-    vec_t<real> t = vzero<real>();
-    for (int c = 0; c < C; c++) {
-      const real *prow = Ptabs[c] + i * KP;
-      for (int e = sg; e < KP; e += G::NSG)
-        t += vsplat<real>(prow[e]) * vld<real>(Mp + ((size_t)c * KP + e) * KP + li * G::VE);
+    if (sgm.first) {
+      vec_t<real> t = vzero<real>();
+      for (int c = 0; c < C; c++) {
+        const real *prow = Ptabs[c] + i * KP;
+        for (int e = sg; e < KP; e += G::NSG)
+          t += vsplat<real>(prow[e]) * vld<real>(Mp + ((size_t)c * KP + e) * KP + li * G::VE);
+      }
+      t = xsg_vsum<G::LPR, real>(t);
+      const real z = a1[i] - (real)r;
+      pk += vsplat<real>((real)w) * (t + vsplat<real>(z) * oQ + bQ);
     }
-    t = xsg_vsum<G::LPR, real>(t);
-    const real z = a1[i] - (real)r;
-    const vec_t<real> out = pk + vsplat<real>((real)w) * (t + vsplat<real>(z) * oQ + bQ);
-    if (sg == 0) vst<real>(h + i * KP + li * G::VE, out);
+    if (sg == 0) vst<real>(h + s * KP + li * G::VE, pk);
   }
 }
 
-// h_i = z_i q1_i, z_i = w (n1 (a_i - r) + sum(b) + sa_i) + sum_pos ((1-w) y~ - w (1-r))
-// (gd_side row body, ffm.cpp:572-589).  One row per wave.
+// Per segment: h[s] = zpart * q1_i, zpart = sum_{p in seg} ((1-w) y~ - w (1-r))
+// + [first] w (n1 (a_i - r) + sum(b) + sa_i)   (gd_side row body, ffm.cpp:572-589).
 template <typename real, int KP>
-__global__ __launch_bounds__(BLOCK) void k_gd_side_row(uint64_t R, const int64_t *__restrict__ yptr,
+__global__ __launch_bounds__(BLOCK) void k_gd_side_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                        const real *__restrict__ yt, const real *__restrict__ Q1,
                                                        const real *__restrict__ a1, const real *__restrict__ sa1,
                                                        const double *__restrict__ bsum, double n1, double w,
@@ -315,34 +340,39 @@ __global__ __launch_bounds__(BLOCK) void k_gd_side_row(uint64_t R, const int64_t
   const int sg = lane / G::LPR, li = lane % G::LPR;
   const real cpos = (real)(1 - w), cneg = (real)(w * (1 - r));
   const double bs = *bsum;
-  for (uint64_t i = wave; i < R; i += nwaves) {
-    real s = 0;
-    for (int64_t p = yptr[i] + lane; p < yptr[i + 1]; p += 64) s += cpos * yt[p] - cneg;
+  for (uint64_t s = wave; s < nseg; s += nwaves) {
+    const Seg sgm = segs[s];
+    const uint64_t i = sgm.row;
+    real z = 0;
+    for (int64_t p = sgm.b + lane; p < sgm.e; p += 64) z += cpos * yt[p] - cneg;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    const real z = (real)(w * (n1 * ((double)a1[i] - r) + bs + (double)sa1[i])) + s;
-    if (sg == 0) vst<real>(h + i * KP + li * G::VE, vsplat<real>(z) * vld<real>(Q1 + i * KP + li * G::VE));
+    for (int o = 32; o > 0; o >>= 1) z += __shfl_xor(z, o, 64);
+    if (sgm.first) z += (real)(w * (n1 * ((double)a1[i] - r) + bs + (double)sa1[i]));
+    if (sg == 0) vst<real>(h + s * KP + li * G::VE, vsplat<real>(z) * vld<real>(Q1 + i * KP + li * G::VE));
   }
 }
 
 // ------------------------------------------------ Hessian-vector rows ---
 // h_i = d_i <phi_i, q1_i> q1_i, phi_i = X_i V, d_i = (1-w)|pos(i)| + w n1
-// (hs_side row body, ffm.cpp:603-624).  One row per subgroup.
+// (hs_side row body, ffm.cpp:603-624).  One row per subgroup, row-indexed h.
 template <typename real, int KP>
 __global__ __launch_bounds__(BLOCK) void k_hs_side_row(uint64_t R, const int64_t *__restrict__ xptr,
                                                        const uint32_t *__restrict__ xidx,
                                                        const real *__restrict__ xval, const real *__restrict__ V,
                                                        const int64_t *__restrict__ yptr,
                                                        const real *__restrict__ Q1, double w, double n1,
-                                                       real *__restrict__ h, const int *__restrict__ run) {
+                                                       real *__restrict__ h, const int *__restrict__ run,
+                                                       const real *__restrict__ Rv, const CgState *st, int it) {
   using G = Geo<real, KP>;
   if (run && !*run) return;
+  const bool upd = st && it > 1;
+  const real beta = upd ? (real)st->beta : (real)0;
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
   for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
     vec_t<real> phi = vzero<real>();
     for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
-      phi += vsplat<real>(xval[p]) * vld<real>(V + (size_t)xidx[p] * KP + li * G::VE);
+      phi += vsplat<real>(xval[p]) * cg_dir_at<real, KP>(V, Rv, beta, upd, (size_t)xidx[p] * KP + li * G::VE);
     const vec_t<real> q = vld<real>(Q1 + i * KP + li * G::VE);
     const real z = sg_sum<G::LPR>(hsum<real>(phi * q));
     const real d = (real)((1 - w) * (double)(yptr[i + 1] - yptr[i]) + w * n1);
@@ -350,19 +380,22 @@ __global__ __launch_bounds__(BLOCK) void k_hs_side_row(uint64_t R, const int64_t
   }
 }
 
-// h_i = (1-w) sum_{j in pos(i)} <phi_i, q_j> q_j + w phi_i QTQ, phi_i = X_i V
-// (hs_cross row body, ffm.cpp:715-738; tau = X_i (V QTQ) = phi_i QTQ).
-// One row per wave; QTQ staged in LDS.
+// Per segment of row i: h[s] = (1-w) sum_{j in seg} <phi_i, q_j> q_j
+// + [first] w phi_i QTQ, phi_i = X_i V  (hs_cross row body, ffm.cpp:715-738;
+// tau = X_i (V QTQ) = phi_i QTQ).  QTQ staged in LDS.
 template <typename real, int KP, bool MLDS>
-__global__ __launch_bounds__(BLOCK) void k_hs_cross_row(uint64_t R, const int64_t *__restrict__ xptr,
+__global__ __launch_bounds__(BLOCK) void k_hs_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
+                                                        const int64_t *__restrict__ xptr,
                                                         const uint32_t *__restrict__ xidx,
                                                         const real *__restrict__ xval, const real *__restrict__ V,
-                                                        const int64_t *__restrict__ yptr,
                                                         const uint32_t *__restrict__ ycol,
                                                         const real *__restrict__ Q1, const real *__restrict__ QTQ,
-                                                        double w, real *__restrict__ h, const int *__restrict__ run) {
+                                                        double w, real *__restrict__ h, const int *__restrict__ run,
+                                                        const real *__restrict__ Rv, const CgState *st, int it) {
   using G = Geo<real, KP>;
   if (run && !*run) return;
+  const bool upd = st && it > 1;
+  const real beta = upd ? (real)st->beta : (real)0;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   real *Qs = reinterpret_cast<real *>(smem_raw);
   real *phis = Qs + (MLDS ? KP * KP : 0);
@@ -376,22 +409,16 @@ __global__ __launch_bounds__(BLOCK) void k_hs_cross_row(uint64_t R, const int64_
   const int sg = lane / G::LPR, li = lane % G::LPR;
   real *myphi = phis + (threadIdx.x >> 6) * KP;
   const real cpos = (real)(1 - w);
-  for (uint64_t i = wave; i < R; i += nwaves) {
+  for (uint64_t s = wave; s < nseg; s += nwaves) {
+    const Seg sgm = segs[s];
+    const uint64_t i = sgm.row;
     vec_t<real> phi = vzero<real>();
     for (int64_t p = xptr[i] + sg; p < xptr[i + 1]; p += G::NSG)
-      phi += vsplat<real>(xval[p]) * vld<real>(V + (size_t)xidx[p] * KP + li * G::VE);
+      phi += vsplat<real>(xval[p]) * cg_dir_at<real, KP>(V, Rv, beta, upd, (size_t)xidx[p] * KP + li * G::VE);
     phi = xsg_vsum<G::LPR, real>(phi);
-    // tau = phi QTQ: subgroup sg handles rows e = sg, sg+NSG, ... of QTQ.
-    if (sg == 0) vst<real>(myphi + li * G::VE, phi);
-    __builtin_amdgcn_wave_barrier();
-    vec_t<real> tau = vzero<real>();
-    for (int e = sg; e < KP; e += G::NSG) tau += vsplat<real>(myphi[e]) * vld<real>(Qp + (size_t)e * KP + li * G::VE);
-    tau = xsg_vsum<G::LPR, real>(tau);
-    __builtin_amdgcn_wave_barrier();
     vec_t<real> ka = vzero<real>();
-    int64_t p = yptr[i] + sg;
-    const int64_t pe = yptr[i + 1];
-    for (; p + G::NSG < pe; p += 2 * G::NSG) {
+    int64_t p = sgm.b + sg;
+    for (; p + G::NSG < sgm.e; p += 2 * G::NSG) {
       const uint32_t j0 = ycol[p], j1 = ycol[p + G::NSG];
       const vec_t<real> q0 = vld<real>(Q1 + (size_t)j0 * KP + li * G::VE);
       const vec_t<real> q1 = vld<real>(Q1 + (size_t)j1 * KP + li * G::VE);
@@ -400,17 +427,31 @@ __global__ __launch_bounds__(BLOCK) void k_hs_cross_row(uint64_t R, const int64_
       ka += vsplat<real>(s0) * q0;
       ka += vsplat<real>(s1) * q1;
     }
-    if (p < pe) {
+    if (p < sgm.e) {
       const vec_t<real> q0 = vld<real>(Q1 + (size_t)ycol[p] * KP + li * G::VE);
       ka += vsplat<real>(sg_sum<G::LPR>(hsum<real>(phi * q0))) * q0;
     }
     ka = xsg_vsum<G::LPR, real>(ka);
-    if (sg == 0) vst<real>(h + i * KP + li * G::VE, vsplat<real>(cpos) * ka + vsplat<real>((real)w) * tau);
+    vec_t<real> out = vsplat<real>(cpos) * ka;
+    if (sgm.first) {
+      // tau = phi QTQ: subgroup sg handles rows e = sg, sg+NSG, ... of QTQ.
+      if (sg == 0) vst<real>(myphi + li * G::VE, phi);
+      __builtin_amdgcn_wave_barrier();
+      vec_t<real> tau = vzero<real>();
+      for (int e = sg; e < KP; e += G::NSG) tau += vsplat<real>(myphi[e]) * vld<real>(Qp + (size_t)e * KP + li * G::VE);
+      tau = xsg_vsum<G::LPR, real>(tau);
+      __builtin_amdgcn_wave_barrier();
+      out += vsplat<real>((real)w) * tau;
+    }
+    if (sg == 0) vst<real>(h + s * KP + li * G::VE, out);
   }
 }
 
 // ---------------------------------------------------------- CSC scatter ---
-// acc[col] (+)= sum_{(row,val) in chunk} val * h[row].  One chunk per subgroup.
+// acc[col] (+)= sum_{(r,val) in chunk} val * h[r].  For segment-mode passes
+// the CSC is built over segments (r = segment id), so a popular row's
+// partials are spread over many chunks instead of one serial sum.
+// One chunk per subgroup; single-chunk columns store, others add atomically.
 template <typename real, int KP>
 __global__ __launch_bounds__(BLOCK) void k_csc(uint64_t nch, const Chunk *__restrict__ ch,
                                                const uint32_t *__restrict__ crow, const real *__restrict__ cval,
@@ -424,19 +465,120 @@ __global__ __launch_bounds__(BLOCK) void k_csc(uint64_t nch, const Chunk *__rest
     const Chunk k = ch[c];
     vec_t<real> s = vzero<real>();
     int64_t p = k.b;
-    for (; p + 1 < k.e; p += 2) {
-      const vec_t<real> h0 = vld<real>(h + (size_t)crow[p] * KP + li * G::VE);
-      const vec_t<real> h1 = vld<real>(h + (size_t)crow[p + 1] * KP + li * G::VE);
+    for (; p + 3 < k.e; p += 4) {
+      const uint32_t r0 = crow[p], r1 = crow[p + 1], r2 = crow[p + 2], r3 = crow[p + 3];
+      const vec_t<real> h0 = vld<real>(h + (size_t)r0 * KP + li * G::VE);
+      const vec_t<real> h1 = vld<real>(h + (size_t)r1 * KP + li * G::VE);
+      const vec_t<real> h2 = vld<real>(h + (size_t)r2 * KP + li * G::VE);
+      const vec_t<real> h3 = vld<real>(h + (size_t)r3 * KP + li * G::VE);
       s += vsplat<real>(cval[p]) * h0;
       s += vsplat<real>(cval[p + 1]) * h1;
+      s += vsplat<real>(cval[p + 2]) * h2;
+      s += vsplat<real>(cval[p + 3]) * h3;
     }
-    if (p < k.e) s += vsplat<real>(cval[p]) * vld<real>(h + (size_t)crow[p] * KP + li * G::VE);
+    for (; p < k.e; p++) s += vsplat<real>(cval[p]) * vld<real>(h + (size_t)crow[p] * KP + li * G::VE);
     real *dst = acc + (size_t)k.col * KP + li * G::VE;
-    if (k.single) {
+    if (k.nch == 1) {
       vst<real>(dst, s);
     } else {
 #pragma unroll
       for (int e = 0; e < G::VE; e++) unsafeAtomicAdd(dst + e, s[e]);
+    }
+  }
+}
+
+// Fused feature pass (single GPU): CSC gather of h per column chunk, then the
+// column's finalisation by its only chunk, or by the last of its chunks to
+// arrive (per-column ticket; partial sums meet in acc through float atomics
+// and are taken back with an atomic exchange that also re-zeroes acc).
+// MODE 0 (gradient, ffm.cpp:561-570, 773-779):
+//   G = lam f W + sum; r = -G; p = r; S = 0; g2 = |G|^2 -> run[1]
+// MODE 1 (Hessian-vector, ffm.cpp:783-805):
+//   p = dir(it); Hp = lam f p + sum; alpha = r2 / <p, Hp>
+template <typename real, int KP, int MODE>
+__global__ __launch_bounds__(BLOCK) void k_feat(int it, uint64_t nch, const Chunk *__restrict__ ch,
+                                                const uint32_t *__restrict__ crow, const real *__restrict__ cval,
+                                                const real *__restrict__ h, real *__restrict__ acc,
+                                                unsigned *__restrict__ cnt, const real *__restrict__ fw, double lam,
+                                                const real *__restrict__ W, real *__restrict__ Gout,
+                                                real *__restrict__ Sv, real *__restrict__ Pv, real *__restrict__ Rv,
+                                                real *__restrict__ Hv, CgState *st, double *part, int *run_host) {
+  using G = Geo<real, KP>;
+  if (MODE == 1 && !st->run[it]) return;
+  const bool upd = MODE == 1 && it > 1;
+  const real beta = upd ? (real)st->beta : (real)0;
+  WAVE_SETUP
+  const int sg = lane / G::LPR, li = lane % G::LPR;
+  double dsum = 0;
+  for (uint64_t c = wave * G::NSG + sg; c < nch; c += nwaves * G::NSG) {
+    const Chunk k = ch[c];
+    vec_t<real> s = vzero<real>();
+    int64_t p = k.b;
+    for (; p + 3 < k.e; p += 4) {
+      const uint32_t r0 = crow[p], r1 = crow[p + 1], r2 = crow[p + 2], r3 = crow[p + 3];
+      const vec_t<real> h0 = vld<real>(h + (size_t)r0 * KP + li * G::VE);
+      const vec_t<real> h1 = vld<real>(h + (size_t)r1 * KP + li * G::VE);
+      const vec_t<real> h2 = vld<real>(h + (size_t)r2 * KP + li * G::VE);
+      const vec_t<real> h3 = vld<real>(h + (size_t)r3 * KP + li * G::VE);
+      s += vsplat<real>(cval[p]) * h0;
+      s += vsplat<real>(cval[p + 1]) * h1;
+      s += vsplat<real>(cval[p + 2]) * h2;
+      s += vsplat<real>(cval[p + 3]) * h3;
+    }
+    for (; p < k.e; p++) s += vsplat<real>(cval[p]) * vld<real>(h + (size_t)crow[p] * KP + li * G::VE);
+    const size_t off = (size_t)k.col * KP + li * G::VE;
+    bool fin = true;
+    if (k.nch > 1) {
+#pragma unroll
+      for (int e = 0; e < G::VE; e++) unsafeAtomicAdd(acc + off + e, s[e]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      unsigned t = 0;
+      if (li == 0) t = __hip_atomic_fetch_add(cnt + k.col, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t = __shfl(t, sg * G::LPR, 64);
+      fin = (t == k.nch - 1);
+      if (fin) {
+#pragma unroll
+        for (int e = 0; e < G::VE; e++)
+          s[e] = __hip_atomic_exchange(acc + off + e, (real)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (li == 0) __hip_atomic_store(cnt + k.col, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (fin) {
+      const real reg = (real)(fw ? lam * (double)fw[k.col] : lam);
+      if (MODE == 0) {
+        const vec_t<real> g = vsplat<real>(reg) * vld<real>(W + off) + s;
+        if (Gout) vst<real>(Gout + off, g);
+        vst<real>(Rv + off, -g);
+        vst<real>(Pv + off, -g);
+        vst<real>(Sv + off, vzero<real>());
+#pragma unroll
+        for (int e = 0; e < G::VE; e++) dsum += (double)g[e] * (double)g[e];
+      } else {
+        const vec_t<real> pe = cg_dir_at<real, KP>(Pv, Rv, beta, upd, off);
+        if (upd) vst<real>(Pv + off, pe);
+        const vec_t<real> hp = vsplat<real>(reg) * pe + s;
+        vst<real>(Hv + off, hp);
+#pragma unroll
+        for (int e = 0; e < G::VE; e++) dsum += (double)pe[e] * (double)hp[e];
+      }
+    }
+  }
+  double bv[1] = {block_sum(dsum)}, tot[1];
+  if (last_block<1>(bv, part, &st->counter, tot) && threadIdx.x == 0) {
+    if (MODE == 0) {
+      st->g2 = tot[0];
+      st->r2 = tot[0];
+      st->nr_cg = 0;
+      for (int i = 0; i <= MAXCG + 1; i++) {
+        st->run[i] = 0;
+        if (run_host) __hip_atomic_store(run_host + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      const int go = (tot[0] * CG_EPS < tot[0]) ? 1 : 0;
+      st->run[1] = go;
+      if (run_host) __hip_atomic_store(run_host + 1, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+      st->vhv = tot[0];
+      st->alpha = st->r2 / tot[0];
     }
   }
 }
@@ -481,17 +623,22 @@ __global__ __launch_bounds__(BLOCK) void k_grad_fin(uint64_t nv, const real *__r
   }
 }
 
-// Hv = lam*freq*V + acc; acc = 0; alpha = r2 / <V,Hv>  (ffm.cpp:783-805).
+// Unfused finalisation (multi-GPU: after the all-reduce of acc):
+// p = dir(it); Hp = lam*freq*p + acc; acc = 0; alpha = r2 / <p,Hp>  (ffm.cpp:783-805).
 template <typename real, int KP>
 __global__ __launch_bounds__(BLOCK) void k_hv_fin(int it, uint64_t nv, const real *__restrict__ fw, double lam,
-                                                  real *__restrict__ acc, const real *__restrict__ Vv,
-                                                  real *__restrict__ Hv, CgState *st, double *part) {
+                                                  real *__restrict__ acc, real *__restrict__ Pv,
+                                                  const real *__restrict__ Rv, real *__restrict__ Hv, CgState *st,
+                                                  double *part) {
   using G = Geo<real, KP>;
   if (!st->run[it]) return;
+  const bool upd = it > 1;
+  const real beta = upd ? (real)st->beta : (real)0;
   double vhv = 0;
   VEC_LOOP {
     const real reg = (real)(fw ? lam * (double)fw[v / G::LPR] : lam);
-    const vec_t<real> x = vld<real>(Vv + v * G::VE);
+    const vec_t<real> x = cg_dir_at<real, KP>(Pv, Rv, beta, upd, v * G::VE);
+    if (upd) vst<real>(Pv + v * G::VE, x);
     const vec_t<real> hv = vsplat<real>(reg) * x + vld<real>(acc + v * G::VE);
     vst<real>(acc + v * G::VE, vzero<real>());
     vst<real>(Hv + v * G::VE, hv);
@@ -533,18 +680,6 @@ __global__ __launch_bounds__(BLOCK) void k_cg_upd(int it, uint64_t nv, const rea
   }
 }
 
-// V = beta V + R  (ffm.cpp:810-811), only when another iteration follows.
-template <typename real, int KP>
-__global__ __launch_bounds__(BLOCK) void k_cg_dir(int it, uint64_t nv, real *__restrict__ Vv,
-                                                  const real *__restrict__ Rv, const CgState *st) {
-  using G = Geo<real, KP>;
-  if (!st->run[it + 1]) return;
-  const real beta = (real)st->beta;
-  VEC_LOOP {
-    vst<real>(Vv + v * G::VE, vsplat<real>(beta) * vld<real>(Vv + v * G::VE) + vld<real>(Rv + v * G::VE));
-  }
-}
-
 // W += S  (ffm.cpp:410, 441).
 template <typename real>
 __global__ __launch_bounds__(BLOCK) void k_axpy1(uint64_t nv, const real *__restrict__ S, real *__restrict__ W) {
@@ -554,14 +689,15 @@ __global__ __launch_bounds__(BLOCK) void k_axpy1(uint64_t nv, const real *__rest
 }
 
 // ------------------------------------------------------- update rows ---
-// XS_i = X_i S; P_i += XS_i; y~_ij += <XS_i, q_j> in both orientations
-// (update_cross, ffm.cpp:439-465).  One row per wave.
+// Per segment of row i: XS_i = X_i S; [first] P_i += XS_i;
+// y~_ij += <XS_i, q_j> for the segment's positives, both orientations
+// (update_cross, ffm.cpp:439-465).
 template <typename real, int KP>
-__global__ __launch_bounds__(BLOCK) void k_update_cross_row(uint64_t R, const int64_t *__restrict__ xptr,
+__global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
+                                                            const int64_t *__restrict__ xptr,
                                                             const uint32_t *__restrict__ xidx,
                                                             const real *__restrict__ xval,
                                                             const real *__restrict__ S, real *__restrict__ P1,
-                                                            const int64_t *__restrict__ yptr,
                                                             const uint32_t *__restrict__ ycol,
                                                             real *__restrict__ yt, real *__restrict__ yt_other,
                                                             const uint32_t *__restrict__ perm,
@@ -569,13 +705,15 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_row(uint64_t R, const in
   using G = Geo<real, KP>;
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
-  for (uint64_t i = wave; i < R; i += nwaves) {
+  for (uint64_t s = wave; s < nseg; s += nwaves) {
+    const Seg sgm = segs[s];
+    const uint64_t i = sgm.row;
     vec_t<real> xs = vzero<real>();
     for (int64_t p = xptr[i] + sg; p < xptr[i + 1]; p += G::NSG)
       xs += vsplat<real>(xval[p]) * vld<real>(S + (size_t)xidx[p] * KP + li * G::VE);
     xs = xsg_vsum<G::LPR, real>(xs);
-    if (sg == 0) vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
-    for (int64_t p = yptr[i] + sg; p < yptr[i + 1]; p += G::NSG) {
+    if (sgm.first && sg == 0) vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
+    for (int64_t p = sgm.b + sg; p < sgm.e; p += G::NSG) {
       const real d = sg_sum<G::LPR>(hsum<real>(xs * vld<real>(Q1 + (size_t)ycol[p] * KP + li * G::VE)));
       if (li == 0) {
         yt[p] += d;
@@ -585,29 +723,34 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_row(uint64_t R, const in
   }
 }
 
-// XS_i = X_i S; P_i += XS_i; gap_i = <XS_i, q1_i>; a_i += gap_i;
-// y~ += gap_i over row i's positives, both orientations (update_side,
-// ffm.cpp:405-437).  One row per wave.
+// Per segment of row i: XS_i = X_i S; gap_i = <XS_i, q1_i>; [first]
+// P_i += XS_i, a_i += gap_i; y~ += gap_i over the segment's positives, both
+// orientations (update_side, ffm.cpp:405-437).
 template <typename real, int KP>
-__global__ __launch_bounds__(BLOCK) void k_update_side_row(uint64_t R, const int64_t *__restrict__ xptr,
+__global__ __launch_bounds__(BLOCK) void k_update_side_seg(uint64_t nseg, const Seg *__restrict__ segs,
+                                                           const int64_t *__restrict__ xptr,
                                                            const uint32_t *__restrict__ xidx,
                                                            const real *__restrict__ xval, const real *__restrict__ S,
                                                            real *__restrict__ P1, const real *__restrict__ Q1,
-                                                           real *__restrict__ a1, const int64_t *__restrict__ yptr,
-                                                           real *__restrict__ yt, real *__restrict__ yt_other,
+                                                           real *__restrict__ a1, real *__restrict__ yt,
+                                                           real *__restrict__ yt_other,
                                                            const uint32_t *__restrict__ perm) {
   using G = Geo<real, KP>;
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
-  for (uint64_t i = wave; i < R; i += nwaves) {
+  for (uint64_t s = wave; s < nseg; s += nwaves) {
+    const Seg sgm = segs[s];
+    const uint64_t i = sgm.row;
     vec_t<real> xs = vzero<real>();
     for (int64_t p = xptr[i] + sg; p < xptr[i + 1]; p += G::NSG)
       xs += vsplat<real>(xval[p]) * vld<real>(S + (size_t)xidx[p] * KP + li * G::VE);
     xs = xsg_vsum<G::LPR, real>(xs);
-    if (sg == 0) vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
     const real gap = sg_sum<G::LPR>(hsum<real>(xs * vld<real>(Q1 + i * KP + li * G::VE)));
-    if (lane == 0) a1[i] += gap;
-    for (int64_t p = yptr[i] + lane; p < yptr[i + 1]; p += 64) {
+    if (sgm.first) {
+      if (sg == 0) vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
+      if (lane == 0) a1[i] += gap;
+    }
+    for (int64_t p = sgm.b + lane; p < sgm.e; p += 64) {
       yt[p] += gap;
       yt_other[perm[p]] += gap;
     }
@@ -615,108 +758,106 @@ __global__ __launch_bounds__(BLOCK) void k_update_side_row(uint64_t R, const int
 }
 
 // ------------------------------------------------- partner aggregates ---
-// Per-block partial sums over rows j of the partner side:
-//   gram[l][e][d] = sum_j A_l[j][e] B[j][d]   (QTQ / Q_ab^T Q1, ffm.cpp:663-670,770)
-// Thread = one 4x4 (e,d) sub-tile of one l; blockIdx.y selects a range of
-// 256 sub-tiles; threads beyond the sub-tile count split the rows.
-template <typename real, int KP>
+// Per-block partial sums over a range of partner rows j:
+//   gram[l][e][d] = sum_j A_l[j][e] B[j][d]     (Q_c^T Q1, ffm.cpp:663-670,770)
+//   col[d]        = sum_j B[j][d]               (oQ = Q1^T 1, ffm.cpp:660)
+//   wcol[d]       = sum_j wv_j B[j][d]          (bQ = Q1^T b, ffm.cpp:661)
+//   wsum          = sum_j wv_j                  (sum of b, ffm.cpp:551)
+// Rows are staged through LDS TR at a time with 16-B cooperative loads (the
+// whole block keeps many loads in flight); each thread then owns up to SPT
+// 4x4 (e,d) sub-tiles and accumulates in registers.  Output layout per block:
+// [L*KP*KP grams | KP col | KP wcol | 1 wsum] (doubles).
+template <typename real, int KP, int SPT>
 __global__ __launch_bounds__(BLOCK) void k_gram_part(uint64_t Rp, int L, const real *const *__restrict__ A,
-                                                     const real *__restrict__ B, double *__restrict__ part,
-                                                     uint64_t rows_per_block) {
-  constexpr int Q4 = (KP >= 4) ? KP / 4 : 1;
-  const int nsub_tot = L * Q4 * Q4;
-  const int sub0 = blockIdx.y * BLOCK;
-  const int nsub = min(BLOCK, nsub_tot - sub0);
-  int groups = 1;
-  while (groups * 2 * nsub <= BLOCK) groups *= 2;
+                                                     const real *__restrict__ B, const real *__restrict__ wv,
+                                                     double *__restrict__ part, uint64_t rows_per_block,
+                                                     int sub_per_y) {
+  constexpr int Q4 = KP / 4;
+  constexpr int TR = (KP >= 64) ? 16 : 32;
+  constexpr int VE = VT<real>::N;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  real *sA = reinterpret_cast<real *>(smem_raw);  // [L][TR][KP]
+  real *sB = sA + (size_t)L * TR * KP;            // [TR][KP]
+  real *sW = sB + (size_t)TR * KP;                // [TR]
   const int t = threadIdx.x;
-  const int g = t / nsub;
-  const int sidx = t % nsub;
-  const bool active = g < groups;
-  const int sub = sub0 + sidx;
-  const int l = sub / (Q4 * Q4);
-  const int eq = (sub / Q4) % Q4;
-  const int dq = sub % Q4;
-  float4 dummy;
-  (void)dummy;
-  double acc[16];
+  const int nsub_tot = L * Q4 * Q4;
+  const int sub0 = blockIdx.y * sub_per_y;
+  const int nsub = max(0, min(sub_per_y, nsub_tot - sub0));
+  real acc[SPT][16];
 #pragma unroll
-  for (int x = 0; x < 16; x++) acc[x] = 0;
+  for (int q = 0; q < SPT; q++)
+#pragma unroll
+    for (int x = 0; x < 16; x++) acc[q][x] = 0;
+  real cs = 0, ws = 0, wtot = 0;
   const uint64_t r0 = (uint64_t)blockIdx.x * rows_per_block;
   const uint64_t r1 = min(Rp, r0 + rows_per_block);
-  if (active) {
-    const real *Al = A[l];
-    for (uint64_t j = r0 + g; j < r1; j += groups) {
-      real av[4], bv[4];
+  const bool do_cols = blockIdx.y == 0;
+  const int pieces_row = KP / VE;
+  const int ntab = L + (B ? 1 : 0);
+  for (uint64_t j0 = r0; j0 < r1; j0 += TR) {
+    const int nr = (int)min<uint64_t>(TR, r1 - j0);
+    __syncthreads();
+    const int tot = ntab * TR * pieces_row;
+    for (int q = t; q < tot; q += BLOCK) {
+      const int tab = q / (TR * pieces_row);
+      const int rr = (q / pieces_row) % TR;
+      const int pc = q % pieces_row;
+      vec_t<real> v = vzero<real>();
+      if (rr < nr) v = vld<real>((tab < L ? A[tab] : B) + (j0 + rr) * KP + pc * VE);
+      vst<real>((tab < L ? sA + ((size_t)tab * TR + rr) * KP : sB + (size_t)rr * KP) + pc * VE, v);
+    }
+    if (wv && t < TR) sW[t] = t < nr ? wv[j0 + t] : (real)0;
+    __syncthreads();
 #pragma unroll
-      for (int x = 0; x < 4; x++) {
-        av[x] = Al[j * KP + eq * 4 + x];
-        bv[x] = B[j * KP + dq * 4 + x];
+    for (int q = 0; q < SPT; q++) {
+      if (t + q * BLOCK < nsub) {
+        const int sub = sub0 + t + q * BLOCK;
+        const int l = sub / (Q4 * Q4), eq = (sub / Q4) % Q4, dq = sub % Q4;
+        const real *pa = sA + (size_t)l * TR * KP + eq * 4;
+        const real *pb = sB + dq * 4;
+        for (int rr = 0; rr < nr; rr++) {
+          real av[4], bv[4];
+#pragma unroll
+          for (int x = 0; x < 4; x++) {
+            av[x] = pa[rr * KP + x];
+            bv[x] = pb[rr * KP + x];
+          }
+#pragma unroll
+          for (int x = 0; x < 4; x++)
+#pragma unroll
+            for (int y = 0; y < 4; y++) acc[q][x * 4 + y] += av[x] * bv[y];
+        }
       }
+    }
+    if (do_cols && t < KP && B) {
+      for (int rr = 0; rr < nr; rr++) {
+        const real bb = sB[rr * KP + t];
+        cs += bb;
+        if (wv) ws += sW[rr] * bb;
+      }
+    }
+    if (do_cols && t == 0 && wv)
+      for (int rr = 0; rr < nr; rr++) wtot += sW[rr];
+  }
+  const size_t NOUT = (size_t)L * KP * KP + 2 * KP + 1;
+  double *out = part + (size_t)blockIdx.x * NOUT;
+#pragma unroll
+  for (int q = 0; q < SPT; q++) {
+    if (t + q * BLOCK < nsub) {
+      const int sub = sub0 + t + q * BLOCK;
+      const int l = sub / (Q4 * Q4), eq = (sub / Q4) % Q4, dq = sub % Q4;
 #pragma unroll
       for (int x = 0; x < 4; x++)
 #pragma unroll
-        for (int y = 0; y < 4; y++) acc[x * 4 + y] += (double)av[x] * (double)bv[y];
+        for (int y = 0; y < 4; y++) out[((size_t)l * KP + eq * 4 + x) * KP + dq * 4 + y] = (double)acc[q][x * 4 + y];
     }
   }
-  // combine row groups in fixed order through LDS
-  __shared__ double sh[BLOCK * 4];
-  const size_t NOUT = (size_t)L * KP * KP;
-  for (int half = 0; half < 4; half++) {
-    __syncthreads();
-    if (active) {
-#pragma unroll
-      for (int y = 0; y < 4; y++) sh[t * 4 + y] = acc[half * 4 + y];
+  if (do_cols) {
+    if (t < KP) {
+      out[(size_t)L * KP * KP + t] = (double)cs;
+      out[(size_t)L * KP * KP + KP + t] = (double)ws;
     }
-    __syncthreads();
-    if (active && g == 0) {
-      double s[4] = {0, 0, 0, 0};
-      for (int gg = 0; gg < groups; gg++)
-#pragma unroll
-        for (int y = 0; y < 4; y++) s[y] += sh[(gg * nsub + sidx) * 4 + y];
-      const int e = eq * 4 + half;
-#pragma unroll
-      for (int y = 0; y < 4; y++) part[(size_t)blockIdx.x * NOUT + ((size_t)l * KP + e) * KP + dq * 4 + y] = s[y];
-    }
-  }
-}
-
-// Column sums over the partner rows: out[0:KP] = sum_j B_j,
-// out[KP:2KP] = sum_j wv_j B_j, out[2KP] = sum_j wv_j (oQ, bQ, sum b).
-template <typename real, int KP>
-__global__ __launch_bounds__(BLOCK) void k_colsum_part(uint64_t Rp, const real *__restrict__ B,
-                                                       const real *__restrict__ wv, double *__restrict__ part,
-                                                       uint64_t rows_per_block) {
-  constexpr int NOUT = 2 * KP + 1;
-  constexpr int LANES = KP < BLOCK ? KP : BLOCK;
-  constexpr int GROUPS = BLOCK / LANES;
-  const int t = threadIdx.x;
-  const int c = t % LANES, g = t / LANES;
-  const uint64_t r0 = (uint64_t)blockIdx.x * rows_per_block;
-  const uint64_t r1 = min(Rp, r0 + rows_per_block);
-  double s0 = 0, s1 = 0, s2 = 0;
-  for (uint64_t j = r0 + g; j < r1; j += GROUPS) {
-    const double wj = wv ? (double)wv[j] : 0.0;
-    const double bj = B ? (double)B[j * KP + c] : 0.0;
-    s0 += bj;
-    s1 += wj * bj;
-    if (c == 0) s2 += wj;
-  }
-  __shared__ double sh[BLOCK * 3];
-  sh[t * 3] = s0;
-  sh[t * 3 + 1] = s1;
-  sh[t * 3 + 2] = s2;
-  __syncthreads();
-  if (g == 0) {
-    double a0 = 0, a1 = 0, a2 = 0;
-    for (int gg = 0; gg < GROUPS; gg++) {
-      a0 += sh[(gg * LANES + c) * 3];
-      a1 += sh[(gg * LANES + c) * 3 + 1];
-      a2 += sh[(gg * LANES + c) * 3 + 2];
-    }
-    part[(size_t)blockIdx.x * NOUT + c] = a0;
-    part[(size_t)blockIdx.x * NOUT + KP + c] = a1;
-    if (c == 0) part[(size_t)blockIdx.x * NOUT + 2 * KP] = a2;
+    if (t == 0) out[(size_t)L * KP * KP + 2 * KP] = (double)wtot;
   }
 }
 
@@ -730,6 +871,17 @@ __global__ __launch_bounds__(BLOCK) void k_reduce_parts(uint64_t nb, uint64_t no
   for (uint64_t b = 0; b < nb; b++) s += part[b * nout + o];
   if (out) out[o] = s;
   if (out_real) out_real[o] = (real)s;
+}
+
+// The 2*KP+1 column-sum outputs stored after `off` in each partial row.
+__global__ __launch_bounds__(BLOCK) void k_reduce_parts_tail(uint64_t nb, uint64_t nout, uint64_t off,
+                                                             const double *__restrict__ part,
+                                                             double *__restrict__ out) {
+  for (uint64_t o = off + threadIdx.x; o < nout; o += BLOCK) {
+    double s = 0;
+    for (uint64_t b = 0; b < nb; b++) s += part[b * nout + o];
+    out[o - off] = s;
+  }
 }
 
 // ------------------------------------------------------- validation ---

@@ -134,6 +134,15 @@ template <typename real> struct DevField {
   DevBuf<real> cval;
   DevBuf<Chunk> chunks;
   DevBuf<real> freqw;  // global feature frequency (for --freq)
+  // the same CSC over positive segments (kernels.hpp: Seg) of the side
+  DevBuf<uint32_t> scrow;
+  DevBuf<real> scval;
+  DevBuf<Chunk> schunks;
+  DevBuf<unsigned> cnt;  // per-column arrival tickets of the fused feature pass (zero at rest)
+  // host copies kept until the segment CSC is built
+  std::vector<int64_t> h_xptr;
+  std::vector<uint32_t> h_xidx;
+  std::vector<double> h_xval;
 };
 
 template <typename real> struct DevSide {
@@ -149,7 +158,68 @@ template <typename real> struct DevSide {
   DevBuf<uint32_t> perm;  // position of the same positive in the other orientation
   DevBuf<real> bias;      // a (users) or b (items)
   DevBuf<real> s;         // sa or sb
+  uint64_t nseg = 0;      // positive segments (kernels.hpp: Seg)
+  DevBuf<Seg> segs;
+  DevBuf<uint32_t> segptr;
 };
+
+// Split every row's positives into segments of at most `len` (rows without
+// positives still get one, empty, segment for their row-local terms).
+template <typename real> static void build_seg_csc(DevSide<real> &s, const std::vector<uint32_t> &segptr) {
+  for (auto &Fp : s.F) {
+    DevField<real> &F = *Fp;
+    const uint64_t R = F.h_xptr.size() - 1;
+    // expand each row's nodes over its segments, then reuse the row builder
+    std::vector<int64_t> xptr(segptr[R] + 1, 0);
+    std::vector<uint32_t> xidx;
+    std::vector<double> xval;
+    uint64_t sidx = 0;
+    for (uint64_t i = 0; i < R; i++)
+      for (uint32_t sg = segptr[i]; sg < segptr[i + 1]; sg++, sidx++) {
+        for (int64_t p = F.h_xptr[i]; p < F.h_xptr[i + 1]; p++) {
+          xidx.push_back(F.h_xidx[p]);
+          xval.push_back(F.h_xval[p]);
+        }
+        xptr[sidx + 1] = (int64_t)xidx.size();
+      }
+    std::vector<uint32_t> crow;
+    std::vector<double> cval;
+    std::vector<Chunk> ch;
+    build_csc(sidx, F.D, xptr.data(), xidx.data(), xval.data(), crow, cval, ch);
+    F.scrow.upload(crow);
+    std::vector<real> cv(cval.begin(), cval.end());
+    F.scval.upload(cv);
+    F.schunks.upload(ch);
+    F.h_xptr.clear();
+    F.h_xptr.shrink_to_fit();
+    F.h_xidx.clear();
+    F.h_xidx.shrink_to_fit();
+    F.h_xval.clear();
+    F.h_xval.shrink_to_fit();
+  }
+}
+
+template <typename real> static void build_segments(DevSide<real> &s, const std::vector<int64_t> &yptr, uint64_t len) {
+  const uint64_t R = yptr.size() - 1;
+  std::vector<Seg> segs;
+  std::vector<uint32_t> segptr(R + 1, 0);
+  segs.reserve(R + (uint64_t)yptr[R] / len + 1);
+  for (uint64_t i = 0; i < R; i++) {
+    segptr[i] = (uint32_t)segs.size();
+    const int64_t b = yptr[i], e = yptr[i + 1];
+    int64_t p = b;
+    do {
+      const int64_t q = std::min<int64_t>(e, p + (int64_t)len);
+      segs.push_back(Seg{(uint32_t)i, p == b ? 1u : 0u, p, q});
+      p = q;
+    } while (p < e);
+  }
+  segptr[R] = (uint32_t)segs.size();
+  s.nseg = segs.size();
+  s.segs.upload(segs);
+  s.segptr.upload(segptr);
+  build_seg_csc(s, segptr);
+}
 
 struct Block {
   bool used = false;
@@ -180,7 +250,8 @@ static void build_csc(uint64_t R, uint64_t D, const int64_t *xptr, const uint32_
     if (e - b <= CH) {
       chunks.push_back(Chunk{(uint32_t)d, 1u, (int64_t)b, (int64_t)e});
     } else {
-      for (uint64_t s = b; s < e; s += CH) chunks.push_back(Chunk{(uint32_t)d, 0u, (int64_t)s, (int64_t)std::min(e, s + CH)});
+      const uint32_t nc = (uint32_t)((e - b + CH - 1) / CH);
+      for (uint64_t s = b; s < e; s += CH) chunks.push_back(Chunk{(uint32_t)d, nc, (int64_t)s, (int64_t)std::min(e, s + CH)});
     }
   }
 }
@@ -237,6 +308,7 @@ template <typename real> class Problem final : public ProblemBase {
       if (j >= V.m) throw Error(OCFFM_E_DATA, "train label >= number of item rows (reference: out-of-bounds read)");
     m_glob_ = U.m;
     n_ = V.m;
+    if (const char *e = std::getenv("OCFFM_SEG_LEN")) seg_len_ = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
     // shard users contiguously
     u0_ = U.m * (uint64_t)comm_.rank / (uint64_t)comm_.nranks;
     u1_ = U.m * (uint64_t)(comm_.rank + 1) / (uint64_t)comm_.nranks;
@@ -269,7 +341,7 @@ template <typename real> class Problem final : public ProblemBase {
     Vd_.alloc(dk);
     Rv_.alloc(dk);
     Hv_.alloc(dk);
-    h_.alloc(std::max<uint64_t>(Rmax, 1) * kp_);
+    h_.alloc(std::max<uint64_t>(std::max(Rmax, std::max(U_.nseg, V_.nseg)), 1) * kp_);
     C_ = fu_ * fv_;
     M_.alloc(std::max<uint32_t>(C_, 1) * kp_ * kp_);
     QTQ_.alloc((size_t)kp_ * kp_);
@@ -372,7 +444,7 @@ template <typename real> class Problem final : public ProblemBase {
       DevSide<real> &out_side = sidew == 0 ? U_ : V_;    // rows scored
       for (uint32_t c = 0; c < C_; c++) {
         real *tab = cross_tab(sidew == 0 ? 1 : 0, c);
-        colsum(part_side.R, tab, nullptr);
+        aggregates(part_side.R, 0, nullptr, tab, nullptr, nullptr);
         HIPCHK(hipMemcpyAsync(vecs_.p + (size_t)c * kp_, sums_.p, kp_ * sizeof(double), hipMemcpyDeviceToDevice, stream_));
       }
       with_kp(kp_, [&](auto K) {
@@ -533,7 +605,7 @@ template <typename real> class Problem final : public ProblemBase {
       for (uint32_t cc = 0; cc < k_; cc++) tmp[rr * kp_ + cc] = (real)v[rr * k_ + cc];
     HIPCHK(hipMemcpyAsync(Vd_.p, tmp.data(), tmp.size() * sizeof(real), hipMemcpyHostToDevice, stream_));
     if (hc.cross) {  // QTQ over the partner rows (slot of this block in the Gram list)
-      gram(hc.partner->R, (int)C_, partner_tabs(hc), hc.Q1, M_.p);
+      aggregates(hc.partner->R, (int)C_, partner_tabs(hc), hc.Q1, nullptr, M_.p);
       const uint32_t c0 = cross_slot(std::min(hc.fl, hc.fo), std::max(hc.fl, hc.fo));
       HIPCHK(hipMemcpyAsync(QTQ_.p, M_.p + (size_t)c0 * kp_ * kp_, (size_t)kp_ * kp_ * sizeof(real),
                             hipMemcpyDeviceToDevice, stream_));
@@ -607,6 +679,10 @@ template <typename real> class Problem final : public ProblemBase {
       F->crow.upload(crow);
       F->cval.upload(to_real(cval));
       F->chunks.upload(ch);
+      F->cnt.alloc(std::max<uint64_t>(F->D, 1));
+      F->h_xptr = std::move(xptr);
+      F->h_xidx = std::move(xidx);
+      F->h_xval = std::move(xval);
       if (prm_.freq && fi < d.f) {  // global counts (all rows, not just this shard)
         std::vector<double> fr(F->D, 0.0);
         for (uint32_t x : d.xidx[fi]) fr[x] += 1;
@@ -627,6 +703,7 @@ template <typename real> class Problem final : public ProblemBase {
     std::vector<uint32_t> ycol(pe - pb);
     for (uint64_t p = pb; p < pe; p++) ycol[p - pb] = (uint32_t)U.ycol[p];
     U_.npos = pe - pb;
+    build_segments(U_, yptr, seg_len_);
     U_.yptr.upload(yptr);
     U_.ycol.upload(ycol);
     U_.yt.alloc(std::max<uint64_t>(U_.npos, 1));
@@ -658,6 +735,7 @@ template <typename real> class Problem final : public ProblemBase {
         v2u[q] = (uint32_t)(p - pb);
       }
     V_.npos = np;
+    build_segments(V_, vptr, seg_len_);
     V_.yptr.upload(vptr);
     V_.ycol.upload(vcol);
     V_.yt.alloc(std::max<uint64_t>(np, 1));
@@ -675,6 +753,11 @@ template <typename real> class Problem final : public ProblemBase {
     T_.row0 = t0;
     std::vector<uint64_t> Ds(U.Ds);  // test fields use the train Ds
     build_fields(T_, Ut, t0, t1, Ds);
+    for (auto &F : T_.F) {
+      F->h_xptr.clear();
+      F->h_xidx.clear();
+      F->h_xval.clear();
+    }
     std::vector<int64_t> lptr(T_.R + 1);
     const uint64_t lb = Ut.yptr[t0];
     for (uint64_t i = 0; i <= T_.R; i++) lptr[i] = (int64_t)(Ut.yptr[t0 + i] - lb);
@@ -817,53 +900,67 @@ template <typename real> class Problem final : public ProblemBase {
     });
   }
 
-  // Column sums over Rp partner rows: sums_[0:KP] = sum B, [KP:2KP] = sum wv*B, [2KP] = sum wv.
-  void colsum(uint64_t Rp, const real *B, const real *wv) {
-    const uint64_t rpb = std::max<uint64_t>(256, (Rp + 255) / 256);
-    const unsigned nb = (unsigned)std::max<uint64_t>(1, (Rp + rpb - 1) / rpb);
-    const uint64_t nout = 2 * kp_ + 1;
-    with_kp(kp_, [&](auto K) {
-      constexpr int KP = decltype(K)::value;
-      prof_launch("colsum", (double)Rp * ((B ? kp_ : 0) + (wv ? 1 : 0)) * sizeof(real), [&] {
-        k_colsum_part<real, KP><<<nb, BLOCK, 0, stream_>>>(Rp, B, wv, part_.p, rpb);
-      });
-    });
-    k_reduce_parts<real><<<grid_for(nout, BLOCK), BLOCK, 0, stream_>>>(nb, nout, part_.p, sums_.p, nullptr);
-    HIPCHK(hipGetLastError());
+  // Partner-side aggregates over Rp rows in one pass (kernels.hpp:
+  // k_gram_part): M (L x KP x KP, real) = A_l^T B for the device pointer
+  // list A, and sums_ = [sum B | sum wv*B | sum wv] (doubles).  A or B or wv
+  // may be absent (L = 0, B = null, wv = null).
+  void aggregates(uint64_t Rp, int L, const real *const *A, const real *B, const real *wv, real *M) {
+    const size_t rs = sizeof(real);
+    const int TR = kp_ >= 64 ? 16 : 32;
+    // tables per launch so the LDS stage fits in 64 KB
+    const int lmax = std::max<int>(1, (int)((64 * 1024 / rs - (size_t)TR * kp_ - TR) / ((size_t)TR * kp_)));
+    int l0 = 0;
+    bool first = true;
+    do {
+      const int Lc = std::min(L - l0, lmax);
+      launch_aggr(Rp, Lc, A ? A + l0 : nullptr, B, first ? wv : nullptr, M ? M + (size_t)l0 * kp_ * kp_ : nullptr,
+                  first);
+      l0 += Lc;
+      first = false;
+    } while (l0 < L);
   }
 
-  // out (L x KP x KP, real) = A_l^T B over Rp partner rows; dev_list is a
-  // device array of L table pointers.
-  void gram(uint64_t Rp, int L, const real *const *dev_list, const real *B, real *out) {
-    const int Q4 = kp_ / 4;
-    const int nsub = L * Q4 * Q4;
-    const unsigned gy = (unsigned)((nsub + BLOCK - 1) / BLOCK);
-    const uint64_t nout = (uint64_t)L * kp_ * kp_;
-    uint64_t nbx = std::min<uint64_t>(256 / std::max<unsigned>(gy, 1) + 1, (Rp + 63) / 64);
-    nbx = std::max<uint64_t>(1, std::min<uint64_t>(nbx, part_.n / std::max<uint64_t>(nout, 1)));
-    const uint64_t rpb = (Rp + nbx - 1) / nbx;
+  void launch_aggr(uint64_t Rp, int L, const real *const *A, const real *B, const real *wv, real *M, bool sums) {
+    const int TR = kp_ >= 64 ? 16 : 32;
+    const size_t smem = ((size_t)L * TR * kp_ + (size_t)TR * kp_ + TR) * sizeof(real);
+    const uint64_t nout = (uint64_t)L * kp_ * kp_ + 2 * kp_ + 1;
+    const int nsub = L * (kp_ / 4) * (kp_ / 4);
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
-      prof_launch("gram", (double)Rp * (L + 1) * kp_ * sizeof(real), [&] {
-        k_gram_part<real, KP><<<dim3((unsigned)nbx, gy), BLOCK, 0, stream_>>>(Rp, L, dev_list, B, part_.p, rpb);
+      constexpr int SPT = KP >= 64 ? 4 : 2;
+      const int sub_per_y = SPT * BLOCK;
+      const unsigned gy = (unsigned)std::max(1, (nsub + sub_per_y - 1) / sub_per_y);
+      uint64_t nbx = std::max<uint64_t>(1, std::min<uint64_t>((Rp + 63) / 64, 512 / gy));
+      nbx = std::min<uint64_t>(nbx, std::max<uint64_t>(1, part_.n / nout));
+      const uint64_t rpb = (Rp + nbx - 1) / nbx;
+      prof_launch("aggregates", (double)Rp * ((L + (B ? 1 : 0)) * kp_ + (wv ? 1 : 0)) * sizeof(real), [&] {
+        k_gram_part<real, KP, SPT><<<dim3((unsigned)nbx, gy), BLOCK, smem, stream_>>>(Rp, L, A, B, wv, part_.p,
+                                                                                      rpb, sub_per_y);
       });
+      const uint64_t ng = (uint64_t)L * KP * KP;
+      if (ng && M)
+        k_reduce_parts<real><<<grid_for(ng, BLOCK, 1u << 20), BLOCK, 0, stream_>>>(nbx, nout, part_.p, nullptr, M);
+      if (sums)
+        k_reduce_parts_tail<<<1, BLOCK, 0, stream_>>>(nbx, nout, ng, part_.p, sums_.p);
+      HIPCHK(hipGetLastError());
     });
-    k_reduce_parts<real><<<grid_for(nout, BLOCK), BLOCK, 0, stream_>>>(nbx, nout, part_.p, nullptr, out);
-    HIPCHK(hipGetLastError());
   }
 
   // CSC scatter of h into acc over one field, then the all-reduce (if any).
-  void scatter(DevField<real> &F, const int *run) {
-    const uint64_t nch = F.chunks.n;
+  // seg: h holds per-segment partials (use the segment CSC of the field).
+  void scatter(DevField<real> &F, const int *run, bool seg) {
+    const uint64_t nch = seg ? F.schunks.n : F.chunks.n;
     if (nch) {
       with_kp(kp_, [&](auto K) {
         constexpr int KP = decltype(K)::value;
         using Gm = Geo<real, KP>;
-        const double bytes = (double)F.nnz * (4 + sizeof(real)) + (double)F.nnz * kp_ * sizeof(real) +
+        const uint64_t ent = seg ? F.scrow.n : F.crow.n;
+        const double bytes = (double)ent * (4 + sizeof(real)) + (double)ent * kp_ * sizeof(real) +
                              (double)F.D * kp_ * sizeof(real) + (double)nch * sizeof(Chunk);
         prof_launch("csc_scatter", bytes, [&] {
-          k_csc<real, KP><<<grid_for(nch, 4 * Gm::NSG), BLOCK, 0, stream_>>>(nch, F.chunks.p, F.crow.p, F.cval.p,
-                                                                             h_.p, acc_.p, run);
+          k_csc<real, KP><<<grid_for(nch, 4 * Gm::NSG), BLOCK, 0, stream_>>>(
+              nch, seg ? F.schunks.p : F.chunks.p, seg ? F.scrow.p : F.crow.p, seg ? F.scval.p : F.cval.p, h_.p,
+              acc_.p, run);
         });
       });
     }
@@ -949,20 +1046,19 @@ template <typename real> class Problem final : public ProblemBase {
       if (h.cross) {
         DevSide<real> &ps = *h.partner;
         // partner aggregates: M_c = A_c^T Q1 for every cross block (A_c = partner-side tables)
-        gram(ps.R, (int)C_, partner_tabs(h), h.Q1, M_.p);
-        colsum(ps.R, h.Q1, ps.bias.p);  // oQ, bQ
+        aggregates(ps.R, (int)C_, partner_tabs(h), h.Q1, ps.bias.p, M_.p);  // M_c, oQ, bQ
         const size_t msz = (size_t)C_ * KP * KP * sizeof(real);
         const bool lds = msz <= 64 * 1024;
         const double bytes = (double)own.R * 8 + (double)own.npos * (4 + rs) + (double)ps.R * KP * rs +
                              (double)C_ * own.R * KP * rs + (double)own.R * rs + (double)own.R * KP * rs;
         prof_launch("gd_cross_row", bytes, [&] {
           if (lds)
-            k_gd_cross_row<real, KP, true><<<grid_for(own.R, 4), BLOCK, msz, stream_>>>(
-                own.R, own.yptr.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
+            k_gd_cross_seg<real, KP, true><<<grid_for(own.nseg, 4), BLOCK, msz, stream_>>>(
+                own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
                 (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, w_, r_, h_.p);
           else
-            k_gd_cross_row<real, KP, false><<<grid_for(own.R, 4), BLOCK, 0, stream_>>>(
-                own.R, own.yptr.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
+            k_gd_cross_seg<real, KP, false><<<grid_for(own.nseg, 4), BLOCK, 0, stream_>>>(
+                own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
                 (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, w_, r_, h_.p);
         });
         // QTQ for CG = M of this block
@@ -971,21 +1067,62 @@ template <typename real> class Problem final : public ProblemBase {
                               hipMemcpyDeviceToDevice, stream_));
       } else {
         DevSide<real> &other = h.user ? V_ : U_;  // sum of the other side's bias (b_sum, ffm.cpp:551)
-        colsum(other.R, nullptr, other.bias.p);
+        aggregates(other.R, 0, nullptr, nullptr, other.bias.p, nullptr);
         const double n1 = (double)other.R;
         const double bytes = (double)own.R * 8 + (double)own.npos * rs + (double)own.R * KP * rs * 2 +
                              (double)own.R * rs * 2;
         prof_launch("gd_side_row", bytes, [&] {
-          k_gd_side_row<real, KP><<<grid_for(own.R, 4), BLOCK, 0, stream_>>>(
-              own.R, own.yptr.p, own.yt.p, h.Q1, own.bias.p, own.s.p, sums_.p + 2 * KP, n1, w_, r_, h_.p);
+          k_gd_side_seg<real, KP><<<grid_for(own.nseg, 4), BLOCK, 0, stream_>>>(
+              own.nseg, own.segs.p, own.yt.p, h.Q1, own.bias.p, own.s.p, sums_.p + 2 * KP, n1, w_, r_, h_.p);
         });
       }
-      scatter(*h.F, nullptr);
+      feature_pass(h, 0, true);
+    });
+  }
+
+  // Feature pass of a half: fused gather + finalisation on one GPU; gather,
+  // all-reduce, finalisation when the partial sums must meet across ranks.
+  // mode 0: gradient (it = 0), mode 1: Hessian-vector of CG iteration `it`.
+  void feature_pass(HalfCtx &h, int it, bool seg) {
+    DevField<real> &F = *h.F;
+    const int *run = it > 0 ? &st_.p->run[it] : nullptr;
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      using Gm = Geo<real, KP>;
+      const double rs = sizeof(real);
       const uint64_t nv = h.D * KP / Gm::VE;
-      prof_launch("grad_fin", (double)h.D * KP * rs * 7, [&] {
-        k_grad_fin<real, KP><<<grid_for(nv, BLOCK, 2048), BLOCK, 0, stream_>>>(
-            nv, h.W1, h.fw, lam_, acc_.p, G_.p, Rv_.p, Vd_.p, S_.p, st_.p, part_.p, run_host_dev_);
-      });
+      if (!comm_.active()) {
+        const uint64_t nch = seg ? F.schunks.n : F.chunks.n;
+        const uint64_t ent = seg ? F.scrow.n : F.crow.n;
+        const double bytes = (double)ent * (4 + rs) + (double)ent * KP * rs + (double)nch * sizeof(Chunk) +
+                             (double)h.D * KP * rs * (it == 0 ? 6 : (it > 1 ? 4 : 2));
+        const unsigned grid = grid_for(nch, 4 * Gm::NSG, 2048);
+        if (it == 0)
+          prof_launch("feat_grad", bytes, [&] {
+            k_feat<real, KP, 0><<<grid, BLOCK, 0, stream_>>>(
+                0, nch, seg ? F.schunks.p : F.chunks.p, seg ? F.scrow.p : F.crow.p, seg ? F.scval.p : F.cval.p, h_.p,
+                acc_.p, F.cnt.p, h.fw, lam_, h.W1, G_.p, S_.p, Vd_.p, Rv_.p, Hv_.p, st_.p, part_.p, run_host_dev_);
+          });
+        else
+          prof_launch("feat_hv", bytes, [&] {
+            k_feat<real, KP, 1><<<grid, BLOCK, 0, stream_>>>(
+                it, nch, seg ? F.schunks.p : F.chunks.p, seg ? F.scrow.p : F.crow.p, seg ? F.scval.p : F.cval.p,
+                h_.p, acc_.p, F.cnt.p, h.fw, lam_, h.W1, G_.p, S_.p, Vd_.p, Rv_.p, Hv_.p, st_.p, part_.p,
+                run_host_dev_);
+          });
+        return;
+      }
+      scatter(F, run, seg);
+      if (it == 0)
+        prof_launch("grad_fin", (double)h.D * KP * rs * 7, [&] {
+          k_grad_fin<real, KP><<<grid_for(nv, BLOCK, 2048), BLOCK, 0, stream_>>>(
+              nv, h.W1, h.fw, lam_, acc_.p, G_.p, Rv_.p, Vd_.p, S_.p, st_.p, part_.p, run_host_dev_);
+        });
+      else
+        prof_launch("hv_fin", (double)h.D * KP * rs * 4, [&] {
+          k_hv_fin<real, KP><<<grid_for(nv, BLOCK, 2048), BLOCK, 0, stream_>>>(it, nv, h.fw, lam_, acc_.p, Vd_.p,
+                                                                              Rv_.p, Hv_.p, st_.p, part_.p);
+        });
     });
   }
 
@@ -1007,11 +1144,13 @@ template <typename real> class Problem final : public ProblemBase {
                                (double)own.npos * 4 + (double)h.partner->R * KP * rs + (double)own.R * KP * rs;
           prof_launch("hs_cross_row", bytes, [&] {
             if (lds)
-              k_hs_cross_row<real, KP, true><<<grid_for(own.R, 4), BLOCK, smem, stream_>>>(
-                  own.R, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.yptr.p, own.ycol.p, h.Q1, QTQ_.p, w_, h_.p, run);
+              k_hs_cross_seg<real, KP, true><<<grid_for(own.nseg, 4), BLOCK, smem, stream_>>>(
+                  own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.ycol.p, h.Q1, QTQ_.p, w_, h_.p,
+                  run, Rv_.p, st_.p, it);
             else
-              k_hs_cross_row<real, KP, false><<<grid_for(own.R, 4), BLOCK, smem, stream_>>>(
-                  own.R, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.yptr.p, own.ycol.p, h.Q1, QTQ_.p, w_, h_.p, run);
+              k_hs_cross_seg<real, KP, false><<<grid_for(own.nseg, 4), BLOCK, smem, stream_>>>(
+                  own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.ycol.p, h.Q1, QTQ_.p, w_, h_.p,
+                  run, Rv_.p, st_.p, it);
           });
         } else {
           DevSide<real> &other = h.user ? V_ : U_;
@@ -1020,17 +1159,12 @@ template <typename real> class Problem final : public ProblemBase {
                                (double)own.R * KP * rs * 2;
           prof_launch("hs_side_row", bytes, [&] {
             k_hs_side_row<real, KP><<<grid_for(own.R, 4 * Gm::NSG), BLOCK, 0, stream_>>>(
-                own.R, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.yptr.p, h.Q1, w_, n1, h_.p, run);
+                own.R, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.yptr.p, h.Q1, w_, n1, h_.p, run, Rv_.p, st_.p, it);
           });
         }
       }
-      scatter(F, run);
-      const uint64_t nv = h.D * KP / Gm::VE;
-      prof_launch("hv_fin", (double)h.D * KP * rs * 4, [&] {
-        k_hv_fin<real, KP><<<grid_for(nv, BLOCK, 2048), BLOCK, 0, stream_>>>(it, nv, h.fw, lam_, acc_.p, Vd_.p,
-                                                                            Hv_.p, st_.p, part_.p);
-      });
     });
+    feature_pass(h, it, h.cross);
   }
 
   void cg_tail(HalfCtx &h, int it) {
@@ -1043,9 +1177,6 @@ template <typename real> class Problem final : public ProblemBase {
         k_cg_upd<real, KP><<<grid_for(nv, BLOCK, 2048), BLOCK, 0, stream_>>>(it, nv, Vd_.p, Hv_.p, S_.p, Rv_.p,
                                                                             st_.p, part_.p, run_host_dev_);
       });
-      prof_launch("cg_dir", (double)h.D * KP * rs * 3, [&] {
-        k_cg_dir<real, KP><<<grid_for(nv, BLOCK, 2048), BLOCK, 0, stream_>>>(it, nv, Vd_.p, Rv_.p, st_.p);
-      });
     });
   }
 
@@ -1053,10 +1184,12 @@ template <typename real> class Problem final : public ProblemBase {
   void half(uint32_t f1, uint32_t f2, int which) {
     HalfCtx h = half_ctx(f1, f2, which);
     gradient(h);
-    // CG with one iteration of look-ahead (see file header).
+    // CG with one iteration of look-ahead (see file header): iteration it is
+    // enqueued before the host waits for iteration it-1's verdict.  The
+    // count of iterations that ran is the last t with run[t] set.
     std::vector<hipEvent_t> evs;
-    int it = 1;
-    for (; it <= MAXCG; it++) {
+    int nr = 0;
+    for (int it = 1; it <= MAXCG; it++) {
       hv_pass(h, it);
       cg_tail(h, it);
       hipEvent_t e = ev();
@@ -1064,11 +1197,14 @@ template <typename real> class Problem final : public ProblemBase {
       evs.push_back(e);
       if (it >= 2) {
         HIPCHK(hipEventSynchronize(evs[it - 2]));
-        if (!__atomic_load_n(&run_host_[it], __ATOMIC_ACQUIRE)) break;  // iteration `it` was a no-op
+        if (!__atomic_load_n(&run_host_[it - 1], __ATOMIC_ACQUIRE)) break;  // it-1 never ran: nr = it-2
+        nr = it - 1;
+        if (!__atomic_load_n(&run_host_[it], __ATOMIC_ACQUIRE)) break;      // iteration it is a no-op
+        nr = it;
       }
     }
     for (auto e : evs) ev_free_.push_back(e);
-    // apply + update (the last verdict is read after the stream drains below)
+    // apply + update
     DevSide<real> &own = *h.own;
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
@@ -1086,8 +1222,8 @@ template <typename real> class Problem final : public ProblemBase {
                              (double)own.R * KP * rs * 2 + (double)own.npos * (4 + 4 + 4 * rs) +
                              (double)other.R * KP * rs;
         prof_launch("update_cross_row", bytes, [&] {
-          k_update_cross_row<real, KP><<<grid_for(own.R, 4), BLOCK, 0, stream_>>>(
-              own.R, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, own.yptr.p, own.ycol.p, own.yt.p, other.yt.p,
+          k_update_cross_seg<real, KP><<<grid_for(own.nseg, 4), BLOCK, 0, stream_>>>(
+              own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, own.ycol.p, own.yt.p, other.yt.p,
               own.perm.p, h.Q1);
         });
       } else {
@@ -1095,17 +1231,12 @@ template <typename real> class Problem final : public ProblemBase {
         const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
                              (double)own.R * KP * rs * 3 + (double)own.R * rs * 2 + (double)own.npos * (4 + 4 * rs);
         prof_launch("update_side_row", bytes, [&] {
-          k_update_side_row<real, KP><<<grid_for(own.R, 4), BLOCK, 0, stream_>>>(
-              own.R, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, h.Q1, own.bias.p, own.yptr.p, own.yt.p,
+          k_update_side_seg<real, KP><<<grid_for(own.nseg, 4), BLOCK, 0, stream_>>>(
+              own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, h.Q1, own.bias.p, own.yt.p,
               other.yt.p, own.perm.p);
         });
       }
     });
-    // CG count of this half: the last iteration that ran
-    HIPCHK(hipStreamSynchronize(stream_));
-    int nr = 0;
-    for (int t = 1; t <= MAXCG; t++)
-      if (__atomic_load_n(&run_host_[t], __ATOMIC_ACQUIRE)) nr = t;
     cg_log.push_back(nr);
     account_half(h, nr);
   }
@@ -1140,6 +1271,7 @@ template <typename real> class Problem final : public ProblemBase {
   uint32_t k_, kp_, fu_, fv_, f_, C_ = 0;
   double w_, lam_, r_;
   uint64_t m_glob_ = 0, n_ = 0, u0_ = 0, u1_ = 0, dmax_ = 0, npop_ = 0;
+  uint64_t seg_len_ = 128;
   DevSide<real> U_, V_, T_;
   std::vector<Block> blocks_;
   std::vector<DevBuf<real>> W_, H_, P_, Q_;

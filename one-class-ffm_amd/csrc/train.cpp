@@ -101,6 +101,10 @@ int main(int argc, char **argv) {
     }
     ocffm_problem *prob = nullptr;
     check(ocffm_problem_create(U, Ut, V, &prm, &prob));
+    // The reference's init is the first consumer of the process rand()
+    // stream (implicit seed 1, ffm.cpp:72); HIP/RCCL start-up above may have
+    // drawn from it, so restore that state before the draws.
+    std::srand(1);
     check(ocffm_problem_init(prob));
     check(ocffm_problem_solve(prob));
     if (!model_path.empty()) check(ocffm_problem_save_model(prob, model_path.c_str()));

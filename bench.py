@@ -110,10 +110,13 @@ def main():
             "launches": d["launches"],
             "epoch_alg_GBps": round(alg / dt / 1e9, 1),
             "epoch_alg_bytes": alg / max(1, args.steps)}
+    # HBM bytes per launch of the same kernel family from the committed
+    # rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, MI355X guide §HBM).
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
-            roof["traffic"] = json.load(open(pmc)).get(dominant)
+            t = json.load(open(pmc)).get(dominant)
+            roof["traffic"] = None if t is None else round(t["bytes_per_launch"])
         except Exception:
             pass
 

@@ -236,8 +236,12 @@ __global__ __launch_bounds__(BLOCK) void k_rowdot_multi(uint64_t R, int C, const
   }
 }
 
-// y~_ij = a_i + b_j + sum_c <P_c[i], Q_c[j]> - 1 for every positive, written
-// to both orientations (init_y_tilde, ffm.cpp:388-403).  One row per wave.
+// y~ is kept factored: the reference maintains y~_ij = a_i + b_j +
+// sum_c <P_c[i], Q_c[j]> - 1 incrementally (init_y_tilde / update_side /
+// update_cross, ffm.cpp:388-465), so only base_ij = sum_c <P_c[i],Q_c[j]> - 1
+// is stored (both orientations) and readers add a_i + b_j.  Side updates then
+// touch no positive at all.  This kernel writes the initial base for every
+// positive (ffm.cpp:388-403).  One row per wave.
 template <typename real, int KP>
 __global__ __launch_bounds__(BLOCK) void k_init_ytilde(uint64_t R, const int64_t *__restrict__ yptr,
                                                        const uint32_t *__restrict__ ycol, real *__restrict__ yt,
@@ -257,7 +261,7 @@ __global__ __launch_bounds__(BLOCK) void k_init_ytilde(uint64_t R, const int64_t
         s += sg_sum<G::LPR>(hsum<real>(vld<real>(Ptabs[c] + i * KP + li * G::VE) *
                                        vld<real>(Qtabs[c] + (size_t)j * KP + li * G::VE)));
       if (li == 0) {
-        const real v = ai + b[j] + s - (real)1;
+        const real v = s - (real)1;  // base_ij; y~_ij = base_ij + a_i + b_j
         yt[p] = v;
         yt_other[perm[p]] = v;
       }
@@ -276,8 +280,8 @@ __global__ __launch_bounds__(BLOCK) void k_gd_cross_seg(uint64_t nseg, const Seg
                                                         const real *__restrict__ yt, const real *__restrict__ Q1,
                                                         int C, const real *const *__restrict__ Ptabs,
                                                         const real *__restrict__ M, const double *__restrict__ sums,
-                                                        const real *__restrict__ a1, double w, double r,
-                                                        real *__restrict__ h) {
+                                                        const real *__restrict__ a1, const real *__restrict__ b1,
+                                                        double w, double r, real *__restrict__ h) {
   using G = Geo<real, KP>;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   real *Ms = reinterpret_cast<real *>(smem_raw);
@@ -300,17 +304,21 @@ __global__ __launch_bounds__(BLOCK) void k_gd_cross_seg(uint64_t nseg, const Seg
   for (uint64_t s = wave; s < nseg; s += nwaves) {
     const Seg sgm = segs[s];
     const uint64_t i = sgm.row;
+    const real ai = a1[i];
     vec_t<real> pk = vzero<real>();
     int64_t p = sgm.b + sg;
     for (; p + G::NSG < sgm.e; p += 2 * G::NSG) {
       const uint32_t j0 = ycol[p], j1 = ycol[p + G::NSG];
-      const real s0 = cpos * yt[p] - cneg, s1 = cpos * yt[p + G::NSG] - cneg;
+      const real s0 = cpos * (yt[p] + ai + b1[j0]) - cneg, s1 = cpos * (yt[p + G::NSG] + ai + b1[j1]) - cneg;
       const vec_t<real> q0 = vld<real>(Q1 + (size_t)j0 * KP + li * G::VE);
       const vec_t<real> q1 = vld<real>(Q1 + (size_t)j1 * KP + li * G::VE);
       pk += vsplat<real>(s0) * q0;
       pk += vsplat<real>(s1) * q1;
     }
-    if (p < sgm.e) pk += vsplat<real>(cpos * yt[p] - cneg) * vld<real>(Q1 + (size_t)ycol[p] * KP + li * G::VE);
+    if (p < sgm.e) {
+      const uint32_t j0 = ycol[p];
+      pk += vsplat<real>(cpos * (yt[p] + ai + b1[j0]) - cneg) * vld<real>(Q1 + (size_t)j0 * KP + li * G::VE);
+    }
     pk = xsg_vsum<G::LPR, real>(pk);
     if (sgm.first) {
       vec_t<real> t = vzero<real>();
@@ -320,7 +328,7 @@ __global__ __launch_bounds__(BLOCK) void k_gd_cross_seg(uint64_t nseg, const Seg
           t += vsplat<real>(prow[e]) * vld<real>(Mp + ((size_t)c * KP + e) * KP + li * G::VE);
       }
       t = xsg_vsum<G::LPR, real>(t);
-      const real z = a1[i] - (real)r;
+      const real z = ai - (real)r;
       pk += vsplat<real>((real)w) * (t + vsplat<real>(z) * oQ + bQ);
     }
     if (sg == 0) vst<real>(h + s * KP + li * G::VE, pk);
@@ -331,8 +339,10 @@ __global__ __launch_bounds__(BLOCK) void k_gd_cross_seg(uint64_t nseg, const Seg
 // + [first] w (n1 (a_i - r) + sum(b) + sa_i)   (gd_side row body, ffm.cpp:572-589).
 template <typename real, int KP>
 __global__ __launch_bounds__(BLOCK) void k_gd_side_seg(uint64_t nseg, const Seg *__restrict__ segs,
+                                                       const uint32_t *__restrict__ ycol,
                                                        const real *__restrict__ yt, const real *__restrict__ Q1,
-                                                       const real *__restrict__ a1, const real *__restrict__ sa1,
+                                                       const real *__restrict__ a1, const real *__restrict__ b1,
+                                                       const real *__restrict__ sa1,
                                                        const double *__restrict__ bsum, double n1, double w,
                                                        double r, real *__restrict__ h) {
   using G = Geo<real, KP>;
@@ -343,11 +353,12 @@ __global__ __launch_bounds__(BLOCK) void k_gd_side_seg(uint64_t nseg, const Seg 
   for (uint64_t s = wave; s < nseg; s += nwaves) {
     const Seg sgm = segs[s];
     const uint64_t i = sgm.row;
+    const real ai = a1[i];
     real z = 0;
-    for (int64_t p = sgm.b + lane; p < sgm.e; p += 64) z += cpos * yt[p] - cneg;
+    for (int64_t p = sgm.b + lane; p < sgm.e; p += 64) z += cpos * (yt[p] + ai + b1[ycol[p]]) - cneg;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) z += __shfl_xor(z, o, 64);
-    if (sgm.first) z += (real)(w * (n1 * ((double)a1[i] - r) + bs + (double)sa1[i]));
+    if (sgm.first) z += (real)(w * (n1 * ((double)ai - r) + bs + (double)sa1[i]));
     if (sg == 0) vst<real>(h + s * KP + li * G::VE, vsplat<real>(z) * vld<real>(Q1 + i * KP + li * G::VE));
   }
 }
@@ -723,37 +734,26 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
   }
 }
 
-// Per segment of row i: XS_i = X_i S; gap_i = <XS_i, q1_i>; [first]
-// P_i += XS_i, a_i += gap_i; y~ += gap_i over the segment's positives, both
-// orientations (update_side, ffm.cpp:405-437).
+// XS_i = X_i S; P_i += XS_i; a_i += <XS_i, q1_i>  (update_side,
+// ffm.cpp:405-437).  The reference also adds the gap to every positive of
+// row i; with y~ kept factored (see k_init_ytilde) that is implied by a_i.
+// One row per subgroup.
 template <typename real, int KP>
-__global__ __launch_bounds__(BLOCK) void k_update_side_seg(uint64_t nseg, const Seg *__restrict__ segs,
-                                                           const int64_t *__restrict__ xptr,
+__global__ __launch_bounds__(BLOCK) void k_update_side_row(uint64_t R, const int64_t *__restrict__ xptr,
                                                            const uint32_t *__restrict__ xidx,
                                                            const real *__restrict__ xval, const real *__restrict__ S,
                                                            real *__restrict__ P1, const real *__restrict__ Q1,
-                                                           real *__restrict__ a1, real *__restrict__ yt,
-                                                           real *__restrict__ yt_other,
-                                                           const uint32_t *__restrict__ perm) {
+                                                           real *__restrict__ a1) {
   using G = Geo<real, KP>;
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
-  for (uint64_t s = wave; s < nseg; s += nwaves) {
-    const Seg sgm = segs[s];
-    const uint64_t i = sgm.row;
+  for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
     vec_t<real> xs = vzero<real>();
-    for (int64_t p = xptr[i] + sg; p < xptr[i + 1]; p += G::NSG)
+    for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
       xs += vsplat<real>(xval[p]) * vld<real>(S + (size_t)xidx[p] * KP + li * G::VE);
-    xs = xsg_vsum<G::LPR, real>(xs);
+    vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
     const real gap = sg_sum<G::LPR>(hsum<real>(xs * vld<real>(Q1 + i * KP + li * G::VE)));
-    if (sgm.first) {
-      if (sg == 0) vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
-      if (lane == 0) a1[i] += gap;
-    }
-    for (int64_t p = sgm.b + lane; p < sgm.e; p += 64) {
-      yt[p] += gap;
-      yt_other[perm[p]] += gap;
-    }
+    if (li == 0) a1[i] += gap;
   }
 }
 
@@ -861,26 +861,34 @@ __global__ __launch_bounds__(BLOCK) void k_gram_part(uint64_t Rp, int L, const r
   }
 }
 
-// out[o] = sum_b part[b][o] in block order; optional real copy.
+// out[o - off] = sum_b part[b][o] for o in [off, off + cnt): a block owns 16
+// consecutive outputs (coalesced 128-B reads) and 16 groups of partial rows;
+// groups are combined in fixed order through LDS (deterministic).
 template <typename real>
-__global__ __launch_bounds__(BLOCK) void k_reduce_parts(uint64_t nb, uint64_t nout, const double *__restrict__ part,
-                                                        double *__restrict__ out, real *__restrict__ out_real) {
-  const uint64_t o = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-  if (o >= nout) return;
+__global__ __launch_bounds__(BLOCK) void k_reduce_parts(uint64_t nb, uint64_t nout, uint64_t off, uint64_t cnt,
+                                                        const double *__restrict__ part, double *__restrict__ out,
+                                                        real *__restrict__ out_real) {
+  __shared__ double sh[16][17];
+  const int to = threadIdx.x & 15, tg = threadIdx.x >> 4;
+  const uint64_t o = (uint64_t)blockIdx.x * 16 + to;
   double s = 0;
-  for (uint64_t b = 0; b < nb; b++) s += part[b * nout + o];
-  if (out) out[o] = s;
-  if (out_real) out_real[o] = (real)s;
-}
-
-// The 2*KP+1 column-sum outputs stored after `off` in each partial row.
-__global__ __launch_bounds__(BLOCK) void k_reduce_parts_tail(uint64_t nb, uint64_t nout, uint64_t off,
-                                                             const double *__restrict__ part,
-                                                             double *__restrict__ out) {
-  for (uint64_t o = off + threadIdx.x; o < nout; o += BLOCK) {
-    double s = 0;
-    for (uint64_t b = 0; b < nb; b++) s += part[b * nout + o];
-    out[o - off] = s;
+  if (o < cnt) {
+    const double *p = part + off + o;
+    uint64_t b = tg;
+    for (; b + 48 < nb; b += 64) {
+      const double x0 = p[b * nout], x1 = p[(b + 16) * nout], x2 = p[(b + 32) * nout], x3 = p[(b + 48) * nout];
+      s += (x0 + x1) + (x2 + x3);
+    }
+    for (; b < nb; b += 16) s += p[b * nout];
+  }
+  sh[tg][to] = s;
+  __syncthreads();
+  if (tg == 0 && o < cnt) {
+    double t = 0;
+#pragma unroll
+    for (int g = 0; g < 16; g++) t += sh[g][to];
+    if (out) out[o] = t;
+    if (out_real) out_real[o] = (real)t;
   }
 }
 

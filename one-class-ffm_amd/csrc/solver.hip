@@ -309,6 +309,7 @@ template <typename real> class Problem final : public ProblemBase {
     m_glob_ = U.m;
     n_ = V.m;
     if (const char *e = std::getenv("OCFFM_SEG_LEN")) seg_len_ = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+    if (const char *e = std::getenv("OCFFM_LOOKAHEAD")) lookahead_ = std::max(1, std::atoi(e));
     // shard users contiguously
     u0_ = U.m * (uint64_t)comm_.rank / (uint64_t)comm_.nranks;
     u1_ = U.m * (uint64_t)(comm_.rank + 1) / (uint64_t)comm_.nranks;
@@ -555,8 +556,8 @@ template <typename real> class Problem final : public ProblemBase {
       case 'b': src = V_.bias.p; rows = V_.R; break;
       case 's': src = U_.s.p; rows = U_.R; break;
       case 't': src = V_.s.p; rows = V_.R; break;
-      case 'u': src = U_.yt.p; rows = U_.npos; break;
-      case 'v': src = V_.yt.p; rows = V_.npos; break;
+      case 'u':
+      case 'v': return get_ytilde(what == 'u', out, cap);
       default: throw Error(OCFFM_E_ARG, "unknown state name");
     }
     const uint64_t count = rows * cols;
@@ -569,6 +570,31 @@ template <typename real> class Problem final : public ProblemBase {
         for (uint64_t cc = 0; cc < cols && o < cap; cc++, o++) out[o] = (double)tmp[rr * stride + cc];
     }
     return count;
+  }
+
+  // y~ = base + a_i + b_j (the factored form, kernels.hpp k_init_ytilde), in
+  // the user-major ('u') or item-major ('v') orientation of this rank.
+  uint64_t get_ytilde(bool user_major, double *out, uint64_t cap) {
+    DevSide<real> &s = user_major ? U_ : V_;
+    const uint64_t np = s.npos;
+    if (!out || !cap) return np;
+    sync();
+    auto down = [&](auto &buf, size_t n) {
+      std::vector<typename std::remove_pointer<decltype(buf.p)>::type> v(n);
+      if (n) HIPCHK(hipMemcpy(v.data(), buf.p, n * sizeof(v[0]), hipMemcpyDeviceToHost));
+      return v;
+    };
+    auto base = down(s.yt, np);
+    auto ptr = down(s.yptr, s.R + 1);
+    auto col = down(s.ycol, np);
+    auto a = down(U_.bias, U_.R);
+    auto b = down(V_.bias, V_.R);
+    for (uint64_t i = 0; i < s.R; i++)
+      for (int64_t p = ptr[i]; p < ptr[i + 1] && (uint64_t)p < cap; p++) {
+        const uint64_t ui = user_major ? i : col[p], vj = user_major ? col[p] : i;
+        out[p] = (double)base[p] + (double)a[ui] + (double)b[vj];
+      }
+    return np;
   }
 
   void set(char what, uint32_t b12, const double *in, uint64_t len) override {
@@ -939,9 +965,15 @@ template <typename real> class Problem final : public ProblemBase {
       });
       const uint64_t ng = (uint64_t)L * KP * KP;
       if (ng && M)
-        k_reduce_parts<real><<<grid_for(ng, BLOCK, 1u << 20), BLOCK, 0, stream_>>>(nbx, nout, part_.p, nullptr, M);
+        prof_launch("aggr_reduce", (double)nbx * ng * 8, [&] {
+          k_reduce_parts<real><<<(unsigned)((ng + 15) / 16), BLOCK, 0, stream_>>>(nbx, nout, 0, ng, part_.p, nullptr,
+                                                                                  M);
+        });
       if (sums)
-        k_reduce_parts_tail<<<1, BLOCK, 0, stream_>>>(nbx, nout, ng, part_.p, sums_.p);
+        prof_launch("aggr_reduce", (double)nbx * (2 * KP + 1) * 8, [&] {
+          k_reduce_parts<real><<<(unsigned)((2 * KP + 1 + 15) / 16), BLOCK, 0, stream_>>>(
+              nbx, nout, ng, 2 * KP + 1, part_.p, sums_.p, nullptr);
+        });
       HIPCHK(hipGetLastError());
     });
   }
@@ -1055,11 +1087,13 @@ template <typename real> class Problem final : public ProblemBase {
           if (lds)
             k_gd_cross_seg<real, KP, true><<<grid_for(own.nseg, 4), BLOCK, msz, stream_>>>(
                 own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
-                (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, w_, r_, h_.p);
+                (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, h.partner->bias.p,
+                w_, r_, h_.p);
           else
             k_gd_cross_seg<real, KP, false><<<grid_for(own.nseg, 4), BLOCK, 0, stream_>>>(
                 own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
-                (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, w_, r_, h_.p);
+                (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, h.partner->bias.p,
+                w_, r_, h_.p);
         });
         // QTQ for CG = M of this block
         const uint32_t c0 = cross_slot(std::min(h.fl, h.fo), std::max(h.fl, h.fo));
@@ -1073,7 +1107,8 @@ template <typename real> class Problem final : public ProblemBase {
                              (double)own.R * rs * 2;
         prof_launch("gd_side_row", bytes, [&] {
           k_gd_side_seg<real, KP><<<grid_for(own.nseg, 4), BLOCK, 0, stream_>>>(
-              own.nseg, own.segs.p, own.yt.p, h.Q1, own.bias.p, own.s.p, sums_.p + 2 * KP, n1, w_, r_, h_.p);
+              own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, own.bias.p, other.bias.p, own.s.p,
+              sums_.p + 2 * KP, n1, w_, r_, h_.p);
         });
       }
       feature_pass(h, 0, true);
@@ -1184,24 +1219,35 @@ template <typename real> class Problem final : public ProblemBase {
   void half(uint32_t f1, uint32_t f2, int which) {
     HalfCtx h = half_ctx(f1, f2, which);
     gradient(h);
-    // CG with one iteration of look-ahead (see file header): iteration it is
-    // enqueued before the host waits for iteration it-1's verdict.  The
-    // count of iterations that ran is the last t with run[t] set.
+    // CG with `lookahead_` iterations in flight (see file header): iteration
+    // it is enqueued before the host waits for iteration it-L's verdict, so
+    // the GPU never waits on the host.  Iterations past the real exit run as
+    // no-ops.  The count of iterations that ran is the last t with run[t].
     std::vector<hipEvent_t> evs;
-    int nr = 0;
-    for (int it = 1; it <= MAXCG; it++) {
+    int nr = 0, known = 0;
+    bool done = false;
+    auto examine = [&](int upto) {
+      for (int q = known + 1; q <= upto && q <= MAXCG && !done; q++) {
+        if (!__atomic_load_n(&run_host_[q], __ATOMIC_ACQUIRE)) done = true;
+        else nr = q;
+        known = q;
+      }
+    };
+    for (int it = 1; it <= MAXCG && !done; it++) {
       hv_pass(h, it);
       cg_tail(h, it);
       hipEvent_t e = ev();
       HIPCHK(hipEventRecord(e, stream_));
       evs.push_back(e);
-      if (it >= 2) {
-        HIPCHK(hipEventSynchronize(evs[it - 2]));
-        if (!__atomic_load_n(&run_host_[it - 1], __ATOMIC_ACQUIRE)) break;  // it-1 never ran: nr = it-2
-        nr = it - 1;
-        if (!__atomic_load_n(&run_host_[it], __ATOMIC_ACQUIRE)) break;      // iteration it is a no-op
-        nr = it;
+      const int t = it - lookahead_;
+      if (t >= 1) {
+        HIPCHK(hipEventSynchronize(evs[t - 1]));
+        examine(t + 1);  // upd(t) decided run[t+1]
       }
+    }
+    if (!done) {
+      HIPCHK(hipEventSynchronize(evs.back()));
+      examine(MAXCG);
     }
     for (auto e : evs) ev_free_.push_back(e);
     // apply + update
@@ -1231,9 +1277,8 @@ template <typename real> class Problem final : public ProblemBase {
         const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
                              (double)own.R * KP * rs * 3 + (double)own.R * rs * 2 + (double)own.npos * (4 + 4 * rs);
         prof_launch("update_side_row", bytes, [&] {
-          k_update_side_seg<real, KP><<<grid_for(own.nseg, 4), BLOCK, 0, stream_>>>(
-              own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, h.Q1, own.bias.p, own.yt.p,
-              other.yt.p, own.perm.p);
+          k_update_side_row<real, KP><<<grid_for(own.R, 4 * Gm::NSG), BLOCK, 0, stream_>>>(
+              own.R, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, h.Q1, own.bias.p);
         });
       }
     });
@@ -1272,6 +1317,7 @@ template <typename real> class Problem final : public ProblemBase {
   double w_, lam_, r_;
   uint64_t m_glob_ = 0, n_ = 0, u0_ = 0, u1_ = 0, dmax_ = 0, npop_ = 0;
   uint64_t seg_len_ = 128;
+  int lookahead_ = 1;
   DevSide<real> U_, V_, T_;
   std::vector<Block> blocks_;
   std::vector<DevBuf<real>> W_, H_, P_, Q_;

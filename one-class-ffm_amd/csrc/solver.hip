@@ -82,7 +82,12 @@ template <typename T> struct DevBuf {
     n = count;
     if (count == 0) return;
     HIPCHK(hipMalloc(&p, count * sizeof(T)));
-    if (zero) HIPCHK(hipMemset(p, 0, count * sizeof(T)));
+    if (zero) {
+      // The solver streams are non-blocking: they do not wait for the legacy
+      // null stream, so the fill must have landed before any kernel runs.
+      HIPCHK(hipMemset(p, 0, count * sizeof(T)));
+      HIPCHK(hipStreamSynchronize(nullptr));
+    }
   }
   void upload(const T *src, size_t count) {
     alloc(count, false);

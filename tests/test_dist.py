@@ -1,0 +1,205 @@
+"""Row-sharded data parallelism.
+
+CPU (world_size 2, gloo): the decomposition the library uses — every
+gradient / Hessian-vector quantity is a sum over users, item-side aggregates
+(oQ, bQ, Grams, n1, sum a, sb) are taken over the local users only, and one
+all-reduce of the D x k partial plus lambda*W once gives the exact result —
+reproduces the oracle's gd_* / hs_* (ffm.cpp:537-742) for every block and half.
+
+GPU: two ranks on one device, all-reduces through the library's host hook
+(gloo), must match a single-rank run (fp64, 1e-9) epoch after epoch.
+"""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle_lib as O
+import synth
+
+WORLD = 2
+
+
+def _dense(rows, nfields, dims):
+    X = [np.zeros((rows.m, dims[f])) for f in range(nfields)]
+    for i in range(rows.m):
+        for p in range(int(rows.xptr[i]), int(rows.xptr[i + 1])):
+            X[int(rows.fid[p])][i, int(rows.idx[p])] += rows.val[p]
+    return X
+
+
+def _problem():
+    ds = synth.general(seed=21, m=40, n=25, fu=2, fv=2, k=4, d_user=[7, 5], d_item=[9, 4], nnz_user=2,
+                       mean_pos=3.0, vals="real")
+    o = O.Oracle(ds, k=4, omega=0.2, lam=0.3, r=-0.7, with_test=False)
+    O.lib().orc_srand(1)
+    o.init()
+    return ds, o
+
+
+def _partials(rank, ds, o):
+    """This rank's partial gradients / Hv products for every half."""
+    k, w, r, lam = o.k, o.omega, o.r, o.lam
+    fu, f, m, n = o.fu, o.f, o.m, o.n
+    du = [int(x) for x in O.data_ds(O.data_from_rows(ds.train))]
+    dv = [int(x) for x in O.data_ds(O.data_from_rows(ds.item))]
+    Xu, Xv = _dense(ds.train, fu, du), _dense(ds.item, o.fv, dv)
+    Y = np.zeros((m, n))
+    for i in range(m):
+        for p in range(int(ds.train.yptr[i]), int(ds.train.yptr[i + 1])):
+            Y[i, int(ds.train.ycol[p])] = 1.0
+    a, b = o.get("a"), o.get("b")
+    u0, u1 = m * rank // WORLD, m * (rank + 1) // WORLD
+    sh = slice(u0, u1)
+    B = lambda f1, f2: O.block_index(f1, f2, f)  # noqa: E731
+    P = {}
+    Q = {}
+    for f1 in range(f):
+        for f2 in range(f1, f):
+            b12 = B(f1, f2)
+            P[b12] = o.get("P", b12).reshape(-1, k)
+            Q[b12] = o.get("Q", b12).reshape(-1, k)
+    cross = [B(f1, f2) for f1 in range(fu) for f2 in range(fu, f)]
+    yt = a[:, None] + b[None, :] + sum(P[c] @ Q[c].T for c in cross) - 1
+    coef = Y * ((1 - w) * yt - w * (1 - r))
+    sa = sum(P[c] @ Q[c].sum(0) for c in cross)
+    sb_loc = sum(Q[c] @ P[c][sh].sum(0) for c in cross)
+    rng = np.random.default_rng(7)
+    out = {}
+    for f1 in range(f):
+        for f2 in range(f1, f):
+            b12 = B(f1, f2)
+            for half in (0, 1):
+                fl = f1 if half == 0 else f2
+                user = fl < fu
+                X = Xu[fl] if user else Xv[fl - fu]
+                D = X.shape[1]
+                Q1 = Q[b12] if half == 0 else P[b12]
+                v = rng.standard_normal((D, k))
+                if (f1 < fu) != (f2 < fu):  # cross
+                    if user:
+                        Xs = X[sh]
+                        oQ, bQ = Q1.sum(0), b @ Q1
+                        T = sum(P[c][sh] @ (Q[c].T @ Q1) for c in cross)
+                        g = coef[sh] @ Q1 + w * (T + (a[sh] - r)[:, None] * oQ + bQ)
+                        QTQ = Q1.T @ Q1
+                        phi = Xs @ v
+                        hv = (1 - w) * (((phi @ Q1.T) * Y[sh]) @ Q1) + w * phi @ QTQ
+                    else:
+                        Xs = X
+                        P1 = Q1[sh]
+                        oQ, bQ = P1.sum(0), a[sh] @ P1
+                        T = sum(Q[c] @ (P[c][sh].T @ P1) for c in cross)
+                        g = coef[sh].T @ P1 + w * (T + (b - r)[:, None] * oQ + bQ)
+                        QTQ = P1.T @ P1
+                        phi = Xs @ v
+                        hv = (1 - w) * (((phi @ P1.T) * Y[sh].T) @ P1) + w * phi @ QTQ
+                else:  # side
+                    if user:
+                        Xs, q = X[sh], Q1[sh]
+                        z = w * (n * (a[sh] - r) + b.sum() + sa[sh]) + coef[sh].sum(1)
+                        d = (1 - w) * Y[sh].sum(1) + w * n
+                    else:
+                        Xs, q = X, Q1
+                        z = w * ((u1 - u0) * (b - r) + a[sh].sum() + sb_loc) + coef[sh].sum(0)
+                        d = (1 - w) * Y[sh].sum(0) + w * (u1 - u0)
+                    g = z[:, None] * q
+                    phi = Xs @ v
+                    hv = (d * (phi * q).sum(1))[:, None] * q
+                out[(b12, half)] = (Xs.T @ g, Xs.T @ hv, v)
+    return out
+
+
+def _worker(rank, port, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    ds, o = _problem()
+    parts = _partials(rank, ds, o)
+    worst = 0.0
+    for (b12, half), (g, hv, v) in sorted(parts.items()):
+        tg = torch.from_numpy(np.ascontiguousarray(g))
+        th = torch.from_numpy(np.ascontiguousarray(hv))
+        dist.all_reduce(tg)
+        dist.all_reduce(th)
+        f1, f2 = [(a, b) for a in range(o.f) for b in range(a, o.f) if O.block_index(a, b, o.f) == b12][0]
+        W = o.get("W" if half == 0 else "H", b12).reshape(-1, o.k)
+        G = tg.numpy() + o.lam * W
+        Hv = th.numpy() + o.lam * v
+        G_ref = o.grad(f1, f2, half).reshape(-1, o.k)
+        H_ref = o.hv(f1, f2, half, v.ravel()).reshape(-1, o.k)
+        worst = max(worst, np.abs(G - G_ref).max() / np.abs(G_ref).max(),
+                    np.abs(Hv - H_ref).max() / np.abs(H_ref).max())
+    if rank == 0:
+        np.save(result_path, np.array([worst]))
+    dist.destroy_process_group()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_sharded_decomposition_gloo():
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "worst.npy")
+        mp.spawn(_worker, args=(_free_port(), path), nprocs=WORLD, join=True)
+        worst = float(np.load(path)[0])
+    assert worst < 1e-10, worst
+
+
+# ------------------------------------------------------------------ GPU ---
+def _gpu_worker(rank, port, out_dir, world):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import ocffm
+
+    def allreduce(arr):
+        t = torch.from_numpy(arr)
+        dist.all_reduce(t)
+
+    ds = synth.tiny(seed=8)
+    g = ocffm.problem_from_dataset(ds, precision=ocffm.FP64, rank=rank, nranks=world, allreduce=allreduce)
+    ocffm.srand(1)
+    g.init()
+    for _ in range(2):
+        g.one_epoch()
+    met = g.validate()
+    W = [g.get("W", b) for b in range(6)] + [g.get("H", b) for b in range(6)]
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), cg=g.cg_log(), loss=met["loss"], ndcg=met["ndcg"],
+             prec=met["prec"], *W)
+    g.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_ranks_match_one_rank_on_gpu():
+    import ocffm
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_gpu_worker, args=(_free_port(), d, WORLD), nprocs=WORLD, join=True)
+        r0 = np.load(os.path.join(d, "r0.npz"))
+        r1 = np.load(os.path.join(d, "r1.npz"))
+        ds = synth.tiny(seed=8)
+        g = ocffm.problem_from_dataset(ds, precision=ocffm.FP64)
+        ocffm.srand(1)
+        g.init()
+        for _ in range(2):
+            g.one_epoch()
+        met = g.validate()
+        np.testing.assert_array_equal(r0["cg"], g.cg_log())
+        np.testing.assert_array_equal(r1["cg"], g.cg_log())
+        for idx, (what, b) in enumerate([("W", b) for b in range(6)] + [("H", b) for b in range(6)]):
+            ref = g.get(what, b)
+            for r in (r0, r1):
+                x = r[f"arr_{idx}"]
+                assert np.abs(x - ref).max() <= 1e-9 * np.abs(ref).max(), (what, b)
+        assert abs(float(r0["loss"]) - met["loss"]) <= 1e-9 * met["loss"]
+        np.testing.assert_allclose(r0["ndcg"], met["ndcg"], atol=1e-12)
+        np.testing.assert_allclose(r0["prec"], met["prec"], atol=1e-12)

@@ -62,9 +62,11 @@ struct Chunk {  // a run of CSC entries of one feature column
 // the CSC pass sums a row's segments in order (deterministic, no atomics).
 struct Seg {
   uint32_t row;
-  uint32_t first;
+  uint32_t info;  // bit 0: first segment of the row; bits 1..: segments of the row
   int64_t b, e;
 };
+__device__ __forceinline__ bool seg_first(const Seg &s) { return s.info & 1u; }
+__device__ __forceinline__ unsigned seg_nrow(const Seg &s) { return s.info >> 1; }
 
 // Device-resident CG scalars (the host never reads them on the hot path).
 struct CgState {
@@ -176,14 +178,135 @@ __device__ __forceinline__ bool last_block(const double (&v)[NV], double *part, 
   (void)lane;                                                                       \
   (void)nwaves;
 
-// CG direction of iteration `it` at feature row d: p_1 = r_0 is stored by
-// the gradient pass; for it > 1 the direction p_it = r + beta p (ffm.cpp:
-// 810-811) is formed on the fly by every reader and stored by the feature
-// pass of iteration it (which owns row d), so no separate direction kernel.
+// CG direction of iteration `it` at feature row d.  The gradient pass stores
+// p_1 = r_0.  The vector update of iteration it-1 (S += a p, r -= a Hp,
+// ffm.cpp:806-807) is applied lazily by the feature pass of iteration it,
+// which owns row d, and every reader of p_it forms it on the fly:
+//   p_it = (r - a_{it-1} Hp_{it-1}) + b_{it-1} p_{it-1}   (ffm.cpp:810-811)
+// with b from |r - a Hp|^2 = r2 - 2a<r,Hp> + a^2|Hp|^2 (same reduction pass).
 template <typename real, int KP>
-__device__ __forceinline__ vec_t<real> cg_dir_at(const real *__restrict__ P, const real *__restrict__ Rv, real beta,
-                                                 bool upd, size_t off) {
-  return upd ? vld<real>(Rv + off) + vsplat<real>(beta) * vld<real>(P + off) : vld<real>(P + off);
+__device__ __forceinline__ vec_t<real> cg_dir_at(const real *__restrict__ P, const real *__restrict__ Rv,
+                                                 const real *__restrict__ Hv, real alpha, real beta, bool upd,
+                                                 size_t off) {
+  if (!upd) return vld<real>(P + off);
+  return (vld<real>(Rv + off) - vsplat<real>(alpha) * vld<real>(Hv + off)) + vsplat<real>(beta) * vld<real>(P + off);
+}
+
+// ------------------------------------------------ column finalisation ---
+// Arguments of the finalisation of a D x k gradient / Hessian-vector column.
+template <typename real> struct Fin {
+  const real *fw;  // per-feature frequency (--freq) or null
+  double lam;
+  const real *W;   // gradient mode: the table being solved
+  real *G;         // gradient mode: G (debug copy) or null
+  real *S, *P, *R, *Hp;
+  real *acc;       // zero at rest; partial sums of multi-part columns
+  unsigned *cnt;   // zero at rest; arrival tickets of multi-part columns
+  CgState *st;
+  double *part;
+  int *run_host;
+  int it;          // CG iteration (Hessian-vector mode)
+};
+
+// A column receiving `nparts` partial sums: each part adds into acc and takes
+// a ticket; the last to arrive gets the total back (atomic exchange also
+// re-zeroes acc) and finalises.  One-part columns finalise directly.
+template <typename real, int KP>
+__device__ __forceinline__ bool col_arrive(const Fin<real> &f, uint32_t col, unsigned nparts, vec_t<real> &s, int sg,
+                                           int li) {
+  using G = Geo<real, KP>;
+  if (nparts <= 1) return true;
+  const size_t off = (size_t)col * KP + li * G::VE;
+#pragma unroll
+  for (int e = 0; e < G::VE; e++) unsafeAtomicAdd(f.acc + off + e, s[e]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  unsigned t = 0;
+  if (li == 0) t = __hip_atomic_fetch_add(f.cnt + col, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  t = __shfl(t, sg * G::LPR, 64);
+  if (t != nparts - 1) return false;
+#pragma unroll
+  for (int e = 0; e < G::VE; e++)
+    s[e] = __hip_atomic_exchange(f.acc + off + e, (real)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (li == 0) __hip_atomic_store(f.cnt + col, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+// MODE 0 (gradient, ffm.cpp:561-570, 773-779): G = lam f W + s; r = -G;
+//   p = r; S = 0; ds[0] += |G|^2.
+// MODE 1 (Hessian-vector, ffm.cpp:783-809): apply iteration it-1's update
+//   (S += a p, r -= a Hp, p = r + b p), then Hp = lam f p + s;
+//   ds += (<p,Hp>, <r,Hp>, |Hp|^2).
+template <typename real, int KP, int MODE>
+__device__ __forceinline__ void col_finalize(const Fin<real> &f, uint32_t col, vec_t<real> s, real alpha, real beta,
+                                             bool upd, int li, double (&ds)[3]) {
+  using G = Geo<real, KP>;
+  const size_t off = (size_t)col * KP + li * G::VE;
+  const real reg = (real)(f.fw ? f.lam * (double)f.fw[col] : f.lam);
+  if (MODE == 0) {
+    const vec_t<real> g = vsplat<real>(reg) * vld<real>(f.W + off) + s;
+    if (f.G) vst<real>(f.G + off, g);
+    vst<real>(f.R + off, -g);
+    vst<real>(f.P + off, -g);
+    vst<real>(f.S + off, vzero<real>());
+#pragma unroll
+    for (int e = 0; e < G::VE; e++) ds[0] += (double)g[e] * (double)g[e];
+  } else {
+    vec_t<real> rn, pe;
+    if (upd) {
+      const vec_t<real> po = vld<real>(f.P + off);
+      rn = vld<real>(f.R + off) - vsplat<real>(alpha) * vld<real>(f.Hp + off);
+      pe = rn + vsplat<real>(beta) * po;
+      vst<real>(f.S + off, vld<real>(f.S + off) + vsplat<real>(alpha) * po);
+      vst<real>(f.R + off, rn);
+      vst<real>(f.P + off, pe);
+    } else {
+      rn = vld<real>(f.R + off);
+      pe = vld<real>(f.P + off);
+    }
+    const vec_t<real> hp = vsplat<real>(reg) * pe + s;
+    vst<real>(f.Hp + off, hp);
+#pragma unroll
+    for (int e = 0; e < G::VE; e++) {
+      ds[0] += (double)pe[e] * (double)hp[e];
+      ds[1] += (double)rn[e] * (double)hp[e];
+      ds[2] += (double)hp[e] * (double)hp[e];
+    }
+  }
+}
+
+// Grid-wide end of a finalising kernel.  MODE 0 publishes g2 and the first
+// CG verdict; MODE 1 computes alpha = r2/<p,Hp>, the new r2 (expanded),
+// beta and the verdict for iteration it+1 (ffm.cpp:780, 803-809).
+template <typename real, int MODE>
+__device__ __forceinline__ void fin_blocks(const Fin<real> &f, const double (&ds)[3]) {
+  double bv[3] = {block_sum(ds[0]), block_sum(ds[1]), block_sum(ds[2])}, tot[3];
+  if (last_block<3>(bv, f.part, &f.st->counter, tot) && threadIdx.x == 0) {
+    CgState *st = f.st;
+    if (MODE == 0) {
+      st->g2 = tot[0];
+      st->r2 = tot[0];
+      st->nr_cg = 0;
+      for (int i = 0; i <= MAXCG + 1; i++) {
+        st->run[i] = 0;
+        if (f.run_host) __hip_atomic_store(f.run_host + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      const int go = (tot[0] * CG_EPS < tot[0]) ? 1 : 0;
+      st->run[1] = go;
+      if (f.run_host) __hip_atomic_store(f.run_host + 1, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+      const double r2 = st->r2;
+      const double alpha = r2 / tot[0];
+      const double r2n = r2 - 2 * alpha * tot[1] + alpha * alpha * tot[2];
+      st->vhv = tot[0];
+      st->alpha = alpha;
+      st->beta = r2n / r2;
+      st->r2 = r2n;
+      st->nr_cg = f.it;
+      const int go = (f.it < MAXCG && st->g2 * CG_EPS < r2n) ? 1 : 0;
+      st->run[f.it + 1] = go;
+      if (f.run_host) __hip_atomic_store(f.run_host + f.it + 1, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // ------------------------------------------------------------------ UTX ---
@@ -270,18 +393,30 @@ __global__ __launch_bounds__(BLOCK) void k_init_ytilde(uint64_t R, const int64_t
 }
 
 // --------------------------------------------------------- gradient rows ---
+// Positive-gather row kernels run ONE SEGMENT PER SUBGROUP (LPR lanes): a
+// wave keeps NSG segments in flight, each walking its (<= 32) positives with
+// 4 independent row gathers per step.  Item rows are short (median ~10
+// positives) and their dependent chain (segment -> row nodes -> feature
+// row -> partner rows) is latency-bound, so parallelism per wave is the lever.
+//
 // Per segment s of row i:
 //   h[s] = sum_{j in seg} ((1-w) y~_ij - w (1-r)) q_j
 //          + [first] w (T_i + (a_i - r) oQ + bQ),   T_i = sum_c P_c[i] M_c
-// (gd_cross row body, ffm.cpp:658-700).  M (C x KP x KP) staged in LDS.
-template <typename real, int KP, bool MLDS>
+// (gd_cross row body, ffm.cpp:658-700); y~ = base + a_i + b_j.  M in LDS.
+// FUSE (id-like field: one node per row, each feature in exactly one row):
+// the CSC is the identity, so instead of writing h the kernel finalises the
+// row's feature column itself (col_arrive / col_finalize, MODE 0).
+template <typename real, int KP, bool MLDS, bool FUSE>
 __global__ __launch_bounds__(BLOCK) void k_gd_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                         const uint32_t *__restrict__ ycol,
                                                         const real *__restrict__ yt, const real *__restrict__ Q1,
                                                         int C, const real *const *__restrict__ Ptabs,
                                                         const real *__restrict__ M, const double *__restrict__ sums,
                                                         const real *__restrict__ a1, const real *__restrict__ b1,
-                                                        double w, double r, real *__restrict__ h) {
+                                                        double w, double r, real *__restrict__ h,
+                                                        const int64_t *__restrict__ xptr,
+                                                        const uint32_t *__restrict__ xidx,
+                                                        const real *__restrict__ xval, Fin<real> f) {
   using G = Geo<real, KP>;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   real *Ms = reinterpret_cast<real *>(smem_raw);
@@ -301,100 +436,132 @@ __global__ __launch_bounds__(BLOCK) void k_gd_cross_seg(uint64_t nseg, const Seg
     oQ[e] = (real)sums[li * G::VE + e];
     bQ[e] = (real)sums[KP + li * G::VE + e];
   }
-  for (uint64_t s = wave; s < nseg; s += nwaves) {
+  double dsum[3] = {0, 0, 0};
+  for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) {
     const Seg sgm = segs[s];
     const uint64_t i = sgm.row;
     const real ai = a1[i];
     vec_t<real> pk = vzero<real>();
-    int64_t p = sgm.b + sg;
-    for (; p + G::NSG < sgm.e; p += 2 * G::NSG) {
-      const uint32_t j0 = ycol[p], j1 = ycol[p + G::NSG];
-      const real s0 = cpos * (yt[p] + ai + b1[j0]) - cneg, s1 = cpos * (yt[p + G::NSG] + ai + b1[j1]) - cneg;
+    int64_t p = sgm.b;
+    for (; p + 3 < sgm.e; p += 4) {
+      const uint32_t j0 = ycol[p], j1 = ycol[p + 1], j2 = ycol[p + 2], j3 = ycol[p + 3];
       const vec_t<real> q0 = vld<real>(Q1 + (size_t)j0 * KP + li * G::VE);
       const vec_t<real> q1 = vld<real>(Q1 + (size_t)j1 * KP + li * G::VE);
-      pk += vsplat<real>(s0) * q0;
-      pk += vsplat<real>(s1) * q1;
+      const vec_t<real> q2 = vld<real>(Q1 + (size_t)j2 * KP + li * G::VE);
+      const vec_t<real> q3 = vld<real>(Q1 + (size_t)j3 * KP + li * G::VE);
+      pk += vsplat<real>(cpos * (yt[p] + ai + b1[j0]) - cneg) * q0;
+      pk += vsplat<real>(cpos * (yt[p + 1] + ai + b1[j1]) - cneg) * q1;
+      pk += vsplat<real>(cpos * (yt[p + 2] + ai + b1[j2]) - cneg) * q2;
+      pk += vsplat<real>(cpos * (yt[p + 3] + ai + b1[j3]) - cneg) * q3;
     }
-    if (p < sgm.e) {
+    for (; p < sgm.e; p++) {
       const uint32_t j0 = ycol[p];
       pk += vsplat<real>(cpos * (yt[p] + ai + b1[j0]) - cneg) * vld<real>(Q1 + (size_t)j0 * KP + li * G::VE);
     }
-    pk = xsg_vsum<G::LPR, real>(pk);
-    if (sgm.first) {
+    if (seg_first(sgm)) {
       vec_t<real> t = vzero<real>();
       for (int c = 0; c < C; c++) {
         const real *prow = Ptabs[c] + i * KP;
-        for (int e = sg; e < KP; e += G::NSG)
-          t += vsplat<real>(prow[e]) * vld<real>(Mp + ((size_t)c * KP + e) * KP + li * G::VE);
+#pragma unroll 4
+        for (int e = 0; e < KP; e++) t += vsplat<real>(prow[e]) * vld<real>(Mp + ((size_t)c * KP + e) * KP + li * G::VE);
       }
-      t = xsg_vsum<G::LPR, real>(t);
       const real z = ai - (real)r;
       pk += vsplat<real>((real)w) * (t + vsplat<real>(z) * oQ + bQ);
     }
-    if (sg == 0) vst<real>(h + s * KP + li * G::VE, pk);
+    if (!FUSE) {
+      vst<real>(h + s * KP + li * G::VE, pk);
+    } else {
+      const int64_t xp = xptr[i];
+      const uint32_t d = xidx[xp];
+      pk = vsplat<real>(xval[xp]) * pk;
+      if (col_arrive<real, KP>(f, d, seg_nrow(sgm), pk, sg, li)) col_finalize<real, KP, 0>(f, d, pk, 0, 0, false, li, dsum);
+    }
   }
+  if (FUSE) fin_blocks<real, 0>(f, dsum);
 }
 
 // Per segment: h[s] = zpart * q1_i, zpart = sum_{p in seg} ((1-w) y~ - w (1-r))
 // + [first] w (n1 (a_i - r) + sum(b) + sa_i)   (gd_side row body, ffm.cpp:572-589).
-template <typename real, int KP>
+template <typename real, int KP, bool FUSE>
 __global__ __launch_bounds__(BLOCK) void k_gd_side_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                        const uint32_t *__restrict__ ycol,
                                                        const real *__restrict__ yt, const real *__restrict__ Q1,
                                                        const real *__restrict__ a1, const real *__restrict__ b1,
                                                        const real *__restrict__ sa1,
                                                        const double *__restrict__ bsum, double n1, double w,
-                                                       double r, real *__restrict__ h) {
+                                                       double r, real *__restrict__ h,
+                                                       const int64_t *__restrict__ xptr,
+                                                       const uint32_t *__restrict__ xidx,
+                                                       const real *__restrict__ xval, Fin<real> f) {
   using G = Geo<real, KP>;
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
   const real cpos = (real)(1 - w), cneg = (real)(w * (1 - r));
   const double bs = *bsum;
-  for (uint64_t s = wave; s < nseg; s += nwaves) {
+  double dsum[3] = {0, 0, 0};
+  for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) {
     const Seg sgm = segs[s];
     const uint64_t i = sgm.row;
     const real ai = a1[i];
     real z = 0;
-    for (int64_t p = sgm.b + lane; p < sgm.e; p += 64) z += cpos * (yt[p] + ai + b1[ycol[p]]) - cneg;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) z += __shfl_xor(z, o, 64);
-    if (sgm.first) z += (real)(w * (n1 * ((double)ai - r) + bs + (double)sa1[i]));
-    if (sg == 0) vst<real>(h + s * KP + li * G::VE, vsplat<real>(z) * vld<real>(Q1 + i * KP + li * G::VE));
+    for (int64_t p = sgm.b + li; p < sgm.e; p += G::LPR) z += cpos * (yt[p] + ai + b1[ycol[p]]) - cneg;
+    z = sg_sum<G::LPR>(z);
+    if (seg_first(sgm)) z += (real)(w * (n1 * ((double)ai - r) + bs + (double)sa1[i]));
+    vec_t<real> out = vsplat<real>(z) * vld<real>(Q1 + i * KP + li * G::VE);
+    if (!FUSE) {
+      vst<real>(h + s * KP + li * G::VE, out);
+    } else {
+      const int64_t xp = xptr[i];
+      const uint32_t d = xidx[xp];
+      out = vsplat<real>(xval[xp]) * out;
+      if (col_arrive<real, KP>(f, d, seg_nrow(sgm), out, sg, li)) col_finalize<real, KP, 0>(f, d, out, 0, 0, false, li, dsum);
+    }
   }
+  if (FUSE) fin_blocks<real, 0>(f, dsum);
 }
 
 // ------------------------------------------------ Hessian-vector rows ---
 // h_i = d_i <phi_i, q1_i> q1_i, phi_i = X_i V, d_i = (1-w)|pos(i)| + w n1
 // (hs_side row body, ffm.cpp:603-624).  One row per subgroup, row-indexed h.
-template <typename real, int KP>
+template <typename real, int KP, bool FUSE>
 __global__ __launch_bounds__(BLOCK) void k_hs_side_row(uint64_t R, const int64_t *__restrict__ xptr,
                                                        const uint32_t *__restrict__ xidx,
                                                        const real *__restrict__ xval, const real *__restrict__ V,
                                                        const int64_t *__restrict__ yptr,
                                                        const real *__restrict__ Q1, double w, double n1,
                                                        real *__restrict__ h, const int *__restrict__ run,
-                                                       const real *__restrict__ Rv, const CgState *st, int it) {
+                                                       const real *__restrict__ Rv, const real *__restrict__ Hv,
+                                                       const CgState *st, int it, Fin<real> f) {
   using G = Geo<real, KP>;
   if (run && !*run) return;
   const bool upd = st && it > 1;
-  const real beta = upd ? (real)st->beta : (real)0;
+  const real alpha = upd ? (real)st->alpha : (real)0, beta = upd ? (real)st->beta : (real)0;
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
+  double dsum[3] = {0, 0, 0};
   for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
     vec_t<real> phi = vzero<real>();
     for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
-      phi += vsplat<real>(xval[p]) * cg_dir_at<real, KP>(V, Rv, beta, upd, (size_t)xidx[p] * KP + li * G::VE);
+      phi += vsplat<real>(xval[p]) * cg_dir_at<real, KP>(V, Rv, Hv, alpha, beta, upd, (size_t)xidx[p] * KP + li * G::VE);
     const vec_t<real> q = vld<real>(Q1 + i * KP + li * G::VE);
     const real z = sg_sum<G::LPR>(hsum<real>(phi * q));
     const real d = (real)((1 - w) * (double)(yptr[i + 1] - yptr[i]) + w * n1);
-    vst<real>(h + i * KP + li * G::VE, vsplat<real>(d * z) * q);
+    const vec_t<real> out = vsplat<real>(d * z) * q;
+    if (!FUSE) {
+      vst<real>(h + i * KP + li * G::VE, out);
+    } else {
+      const int64_t xp = xptr[i];
+      col_finalize<real, KP, 1>(f, xidx[xp], vsplat<real>(xval[xp]) * out, alpha, beta, upd, li, dsum);
+    }
   }
+  if (FUSE) fin_blocks<real, 1>(f, dsum);
 }
 
 // Per segment of row i: h[s] = (1-w) sum_{j in seg} <phi_i, q_j> q_j
-// + [first] w phi_i QTQ, phi_i = X_i V  (hs_cross row body, ffm.cpp:715-738;
-// tau = X_i (V QTQ) = phi_i QTQ).  QTQ staged in LDS.
-template <typename real, int KP, bool MLDS>
+// + [first] w phi_i QTQ, phi_i = X_i p  (hs_cross row body, ffm.cpp:715-738;
+// tau = X_i (V QTQ) = phi_i QTQ).  QTQ staged in LDS; phi of a first
+// segment staged per subgroup for the broadcast reads of the k x k product.
+template <typename real, int KP, bool MLDS, bool FUSE>
 __global__ __launch_bounds__(BLOCK) void k_hs_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                         const int64_t *__restrict__ xptr,
                                                         const uint32_t *__restrict__ xidx,
@@ -402,11 +569,12 @@ __global__ __launch_bounds__(BLOCK) void k_hs_cross_seg(uint64_t nseg, const Seg
                                                         const uint32_t *__restrict__ ycol,
                                                         const real *__restrict__ Q1, const real *__restrict__ QTQ,
                                                         double w, real *__restrict__ h, const int *__restrict__ run,
-                                                        const real *__restrict__ Rv, const CgState *st, int it) {
+                                                        const real *__restrict__ Rv, const real *__restrict__ Hv,
+                                                        const CgState *st, int it, Fin<real> f) {
   using G = Geo<real, KP>;
   if (run && !*run) return;
   const bool upd = st && it > 1;
-  const real beta = upd ? (real)st->beta : (real)0;
+  const real alpha = upd ? (real)st->alpha : (real)0, beta = upd ? (real)st->beta : (real)0;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   real *Qs = reinterpret_cast<real *>(smem_raw);
   real *phis = Qs + (MLDS ? KP * KP : 0);
@@ -418,44 +586,56 @@ __global__ __launch_bounds__(BLOCK) void k_hs_cross_seg(uint64_t nseg, const Seg
   }
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
-  real *myphi = phis + (threadIdx.x >> 6) * KP;
+  real *myphi = phis + (threadIdx.x / G::LPR) * KP;
   const real cpos = (real)(1 - w);
-  for (uint64_t s = wave; s < nseg; s += nwaves) {
+  double dsum[3] = {0, 0, 0};
+  for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) {
     const Seg sgm = segs[s];
     const uint64_t i = sgm.row;
     vec_t<real> phi = vzero<real>();
-    for (int64_t p = xptr[i] + sg; p < xptr[i + 1]; p += G::NSG)
-      phi += vsplat<real>(xval[p]) * cg_dir_at<real, KP>(V, Rv, beta, upd, (size_t)xidx[p] * KP + li * G::VE);
-    phi = xsg_vsum<G::LPR, real>(phi);
+    for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
+      phi += vsplat<real>(xval[p]) * cg_dir_at<real, KP>(V, Rv, Hv, alpha, beta, upd, (size_t)xidx[p] * KP + li * G::VE);
     vec_t<real> ka = vzero<real>();
-    int64_t p = sgm.b + sg;
-    for (; p + G::NSG < sgm.e; p += 2 * G::NSG) {
-      const uint32_t j0 = ycol[p], j1 = ycol[p + G::NSG];
+    int64_t p = sgm.b;
+    for (; p + 3 < sgm.e; p += 4) {
+      const uint32_t j0 = ycol[p], j1 = ycol[p + 1], j2 = ycol[p + 2], j3 = ycol[p + 3];
       const vec_t<real> q0 = vld<real>(Q1 + (size_t)j0 * KP + li * G::VE);
       const vec_t<real> q1 = vld<real>(Q1 + (size_t)j1 * KP + li * G::VE);
+      const vec_t<real> q2 = vld<real>(Q1 + (size_t)j2 * KP + li * G::VE);
+      const vec_t<real> q3 = vld<real>(Q1 + (size_t)j3 * KP + li * G::VE);
       const real s0 = sg_sum<G::LPR>(hsum<real>(phi * q0));
       const real s1 = sg_sum<G::LPR>(hsum<real>(phi * q1));
+      const real s2 = sg_sum<G::LPR>(hsum<real>(phi * q2));
+      const real s3 = sg_sum<G::LPR>(hsum<real>(phi * q3));
       ka += vsplat<real>(s0) * q0;
       ka += vsplat<real>(s1) * q1;
+      ka += vsplat<real>(s2) * q2;
+      ka += vsplat<real>(s3) * q3;
     }
-    if (p < sgm.e) {
+    for (; p < sgm.e; p++) {
       const vec_t<real> q0 = vld<real>(Q1 + (size_t)ycol[p] * KP + li * G::VE);
       ka += vsplat<real>(sg_sum<G::LPR>(hsum<real>(phi * q0))) * q0;
     }
-    ka = xsg_vsum<G::LPR, real>(ka);
     vec_t<real> out = vsplat<real>(cpos) * ka;
-    if (sgm.first) {
-      // tau = phi QTQ: subgroup sg handles rows e = sg, sg+NSG, ... of QTQ.
-      if (sg == 0) vst<real>(myphi + li * G::VE, phi);
+    if (seg_first(sgm)) {
+      vst<real>(myphi + li * G::VE, phi);
       __builtin_amdgcn_wave_barrier();
       vec_t<real> tau = vzero<real>();
-      for (int e = sg; e < KP; e += G::NSG) tau += vsplat<real>(myphi[e]) * vld<real>(Qp + (size_t)e * KP + li * G::VE);
-      tau = xsg_vsum<G::LPR, real>(tau);
+#pragma unroll 4
+      for (int e = 0; e < KP; e++) tau += vsplat<real>(myphi[e]) * vld<real>(Qp + (size_t)e * KP + li * G::VE);
       __builtin_amdgcn_wave_barrier();
       out += vsplat<real>((real)w) * tau;
     }
-    if (sg == 0) vst<real>(h + s * KP + li * G::VE, out);
+    if (!FUSE) {
+      vst<real>(h + s * KP + li * G::VE, out);
+    } else {
+      const int64_t xp = xptr[i];
+      const uint32_t d = xidx[xp];
+      out = vsplat<real>(xval[xp]) * out;
+      if (col_arrive<real, KP>(f, d, seg_nrow(sgm), out, sg, li)) col_finalize<real, KP, 1>(f, d, out, alpha, beta, upd, li, dsum);
+    }
   }
+  if (FUSE) fin_blocks<real, 1>(f, dsum);
 }
 
 // ---------------------------------------------------------- CSC scatter ---
@@ -499,28 +679,19 @@ __global__ __launch_bounds__(BLOCK) void k_csc(uint64_t nch, const Chunk *__rest
 }
 
 // Fused feature pass (single GPU): CSC gather of h per column chunk, then the
-// column's finalisation by its only chunk, or by the last of its chunks to
-// arrive (per-column ticket; partial sums meet in acc through float atomics
-// and are taken back with an atomic exchange that also re-zeroes acc).
-// MODE 0 (gradient, ffm.cpp:561-570, 773-779):
-//   G = lam f W + sum; r = -G; p = r; S = 0; g2 = |G|^2 -> run[1]
-// MODE 1 (Hessian-vector, ffm.cpp:783-805):
-//   p = dir(it); Hp = lam f p + sum; alpha = r2 / <p, Hp>
+// column's finalisation by its only chunk or by the last of its chunks
+// (col_arrive / col_finalize above).
 template <typename real, int KP, int MODE>
-__global__ __launch_bounds__(BLOCK) void k_feat(int it, uint64_t nch, const Chunk *__restrict__ ch,
+__global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nch, const Chunk *__restrict__ ch,
                                                 const uint32_t *__restrict__ crow, const real *__restrict__ cval,
-                                                const real *__restrict__ h, real *__restrict__ acc,
-                                                unsigned *__restrict__ cnt, const real *__restrict__ fw, double lam,
-                                                const real *__restrict__ W, real *__restrict__ Gout,
-                                                real *__restrict__ Sv, real *__restrict__ Pv, real *__restrict__ Rv,
-                                                real *__restrict__ Hv, CgState *st, double *part, int *run_host) {
+                                                const real *__restrict__ h, Fin<real> f) {
   using G = Geo<real, KP>;
-  if (MODE == 1 && !st->run[it]) return;
-  const bool upd = MODE == 1 && it > 1;
-  const real beta = upd ? (real)st->beta : (real)0;
+  if (MODE == 1 && !f.st->run[f.it]) return;
+  const bool upd = MODE == 1 && f.it > 1;
+  const real alpha = upd ? (real)f.st->alpha : (real)0, beta = upd ? (real)f.st->beta : (real)0;
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
-  double dsum = 0;
+  double dsum[3] = {0, 0, 0};
   for (uint64_t c = wave * G::NSG + sg; c < nch; c += nwaves * G::NSG) {
     const Chunk k = ch[c];
     vec_t<real> s = vzero<real>();
@@ -537,172 +708,51 @@ __global__ __launch_bounds__(BLOCK) void k_feat(int it, uint64_t nch, const Chun
       s += vsplat<real>(cval[p + 3]) * h3;
     }
     for (; p < k.e; p++) s += vsplat<real>(cval[p]) * vld<real>(h + (size_t)crow[p] * KP + li * G::VE);
-    const size_t off = (size_t)k.col * KP + li * G::VE;
-    bool fin = true;
-    if (k.nch > 1) {
-#pragma unroll
-      for (int e = 0; e < G::VE; e++) unsafeAtomicAdd(acc + off + e, s[e]);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      unsigned t = 0;
-      if (li == 0) t = __hip_atomic_fetch_add(cnt + k.col, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      t = __shfl(t, sg * G::LPR, 64);
-      fin = (t == k.nch - 1);
-      if (fin) {
-#pragma unroll
-        for (int e = 0; e < G::VE; e++)
-          s[e] = __hip_atomic_exchange(acc + off + e, (real)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (li == 0) __hip_atomic_store(cnt + k.col, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    if (fin) {
-      const real reg = (real)(fw ? lam * (double)fw[k.col] : lam);
-      if (MODE == 0) {
-        const vec_t<real> g = vsplat<real>(reg) * vld<real>(W + off) + s;
-        if (Gout) vst<real>(Gout + off, g);
-        vst<real>(Rv + off, -g);
-        vst<real>(Pv + off, -g);
-        vst<real>(Sv + off, vzero<real>());
-#pragma unroll
-        for (int e = 0; e < G::VE; e++) dsum += (double)g[e] * (double)g[e];
-      } else {
-        const vec_t<real> pe = cg_dir_at<real, KP>(Pv, Rv, beta, upd, off);
-        if (upd) vst<real>(Pv + off, pe);
-        const vec_t<real> hp = vsplat<real>(reg) * pe + s;
-        vst<real>(Hv + off, hp);
-#pragma unroll
-        for (int e = 0; e < G::VE; e++) dsum += (double)pe[e] * (double)hp[e];
-      }
-    }
+    if (col_arrive<real, KP>(f, k.col, k.nch, s, sg, li)) col_finalize<real, KP, MODE>(f, k.col, s, alpha, beta, upd, li, dsum);
   }
-  double bv[1] = {block_sum(dsum)}, tot[1];
-  if (last_block<1>(bv, part, &st->counter, tot) && threadIdx.x == 0) {
-    if (MODE == 0) {
-      st->g2 = tot[0];
-      st->r2 = tot[0];
-      st->nr_cg = 0;
-      for (int i = 0; i <= MAXCG + 1; i++) {
-        st->run[i] = 0;
-        if (run_host) __hip_atomic_store(run_host + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-      const int go = (tot[0] * CG_EPS < tot[0]) ? 1 : 0;
-      st->run[1] = go;
-      if (run_host) __hip_atomic_store(run_host + 1, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    } else {
-      st->vhv = tot[0];
-      st->alpha = st->r2 / tot[0];
-    }
-  }
+  fin_blocks<real, MODE>(f, dsum);
 }
 
 // ------------------------------------------------- CG vector kernels ---
 // All operate on n vectors of VE elements (D x KP buffers); row = v / LPR.
 #define VEC_LOOP for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < nv; v += (uint64_t)gridDim.x * BLOCK)
 
-__device__ __forceinline__ void publish_run(CgState *st, int *run_host, int idx, int val) {
-  st->run[idx] = val;
-  if (run_host) __hip_atomic_store(run_host + idx, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// G = lam*freq*W + acc; acc = 0; R = -G; V = R; S = 0; g2 = |G|^2
-// (ffm.cpp:561-570 regulariser, 773-779 CG start).
-template <typename real, int KP>
-__global__ __launch_bounds__(BLOCK) void k_grad_fin(uint64_t nv, const real *__restrict__ W,
-                                                    const real *__restrict__ fw, double lam, real *__restrict__ acc,
-                                                    real *__restrict__ Gout, real *__restrict__ Rv,
-                                                    real *__restrict__ Vv, real *__restrict__ Sv, CgState *st,
-                                                    double *part, int *run_host) {
+// Unfused finalisation (multi-GPU: after the all-reduce of acc), the same
+// col_finalize / fin_blocks as the fused feature pass with s = acc (then
+// acc = 0).  MODE 0: gradient start (ffm.cpp:561-570, 773-779); MODE 1:
+// Hessian-vector product of CG iteration f.it (ffm.cpp:783-809).
+template <typename real, int KP, int MODE>
+__global__ __launch_bounds__(BLOCK) void k_fin(uint64_t nv, Fin<real> f) {
   using G = Geo<real, KP>;
-  double g2 = 0;
+  if (MODE == 1 && !f.st->run[f.it]) return;
+  const bool upd = MODE == 1 && f.it > 1;
+  const real alpha = upd ? (real)f.st->alpha : (real)0, beta = upd ? (real)f.st->beta : (real)0;
+  double dsum[3] = {0, 0, 0};
   VEC_LOOP {
-    const real reg = (real)(fw ? lam * (double)fw[v / G::LPR] : lam);
-    const vec_t<real> g = vsplat<real>(reg) * vld<real>(W + v * G::VE) + vld<real>(acc + v * G::VE);
-    vst<real>(acc + v * G::VE, vzero<real>());
-    if (Gout) vst<real>(Gout + v * G::VE, g);
-    vst<real>(Rv + v * G::VE, -g);
-    vst<real>(Vv + v * G::VE, -g);
-    vst<real>(Sv + v * G::VE, vzero<real>());
-#pragma unroll
-    for (int e = 0; e < G::VE; e++) g2 += (double)g[e] * (double)g[e];
+    const vec_t<real> s = vld<real>(f.acc + v * G::VE);
+    vst<real>(f.acc + v * G::VE, vzero<real>());
+    col_finalize<real, KP, MODE>(f, (uint32_t)(v / G::LPR), s, alpha, beta, upd, (int)(v % G::LPR), dsum);
   }
-  double bv[1] = {block_sum(g2)}, tot[1];
-  if (last_block<1>(bv, part, &st->counter, tot) && threadIdx.x == 0) {
-    st->g2 = tot[0];
-    st->r2 = tot[0];
-    st->nr_cg = 0;
-    for (int it = 0; it <= MAXCG + 1; it++) publish_run(st, run_host, it, 0);
-    publish_run(st, run_host, 1, (tot[0] * CG_EPS < tot[0]) ? 1 : 0);
-  }
+  fin_blocks<real, MODE>(f, dsum);
 }
 
-// Unfused finalisation (multi-GPU: after the all-reduce of acc):
-// p = dir(it); Hp = lam*freq*p + acc; acc = 0; alpha = r2 / <p,Hp>  (ffm.cpp:783-805).
-template <typename real, int KP>
-__global__ __launch_bounds__(BLOCK) void k_hv_fin(int it, uint64_t nv, const real *__restrict__ fw, double lam,
-                                                  real *__restrict__ acc, real *__restrict__ Pv,
-                                                  const real *__restrict__ Rv, real *__restrict__ Hv, CgState *st,
-                                                  double *part) {
-  using G = Geo<real, KP>;
-  if (!st->run[it]) return;
-  const bool upd = it > 1;
-  const real beta = upd ? (real)st->beta : (real)0;
-  double vhv = 0;
-  VEC_LOOP {
-    const real reg = (real)(fw ? lam * (double)fw[v / G::LPR] : lam);
-    const vec_t<real> x = cg_dir_at<real, KP>(Pv, Rv, beta, upd, v * G::VE);
-    if (upd) vst<real>(Pv + v * G::VE, x);
-    const vec_t<real> hv = vsplat<real>(reg) * x + vld<real>(acc + v * G::VE);
-    vst<real>(acc + v * G::VE, vzero<real>());
-    vst<real>(Hv + v * G::VE, hv);
-#pragma unroll
-    for (int e = 0; e < G::VE; e++) vhv += (double)x[e] * (double)hv[e];
-  }
-  double bv[1] = {block_sum(vhv)}, tot[1];
-  if (last_block<1>(bv, part, &st->counter, tot) && threadIdx.x == 0) {
-    st->vhv = tot[0];
-    st->alpha = st->r2 / tot[0];
-  }
-}
-
-// S += alpha V; R -= alpha Hv; r2' = |R|^2; beta = r2'/r2  (ffm.cpp:804-809)
-// and the loop test g2*eps < r2 && it < 20 (ffm.cpp:780).
-template <typename real, int KP>
-__global__ __launch_bounds__(BLOCK) void k_cg_upd(int it, uint64_t nv, const real *__restrict__ Vv,
-                                                  const real *__restrict__ Hv, real *__restrict__ Sv,
-                                                  real *__restrict__ Rv, CgState *st, double *part, int *run_host) {
-  using G = Geo<real, KP>;
-  if (!st->run[it]) return;
-  const real alpha = (real)st->alpha;
-  double r2 = 0;
-  VEC_LOOP {
-    const vec_t<real> s = vld<real>(Sv + v * G::VE) + vsplat<real>(alpha) * vld<real>(Vv + v * G::VE);
-    const vec_t<real> rr = vld<real>(Rv + v * G::VE) - vsplat<real>(alpha) * vld<real>(Hv + v * G::VE);
-    vst<real>(Sv + v * G::VE, s);
-    vst<real>(Rv + v * G::VE, rr);
-#pragma unroll
-    for (int e = 0; e < G::VE; e++) r2 += (double)rr[e] * (double)rr[e];
-  }
-  double bv[1] = {block_sum(r2)}, tot[1];
-  if (last_block<1>(bv, part, &st->counter, tot) && threadIdx.x == 0) {
-    const double gamma = st->r2;
-    st->beta = tot[0] / gamma;
-    st->r2 = tot[0];
-    st->nr_cg = it;
-    publish_run(st, run_host, it + 1, (it < MAXCG && st->g2 * CG_EPS < tot[0]) ? 1 : 0);
-  }
-}
-
-// W += S  (ffm.cpp:410, 441).
+// The step of the half: S += alpha_last p_last (the update of the last CG
+// iteration, pending under the lazy scheme above), W += S  (ffm.cpp:806, 410, 441).
 template <typename real>
-__global__ __launch_bounds__(BLOCK) void k_axpy1(uint64_t nv, const real *__restrict__ S, real *__restrict__ W) {
+__global__ __launch_bounds__(BLOCK) void k_apply(uint64_t nv, const real *__restrict__ P, real *__restrict__ S,
+                                                 real *__restrict__ W, const CgState *st) {
+  const real alpha = st->nr_cg >= 1 ? (real)st->alpha : (real)0;
   VEC_LOOP {
-    vst<real>(W + v * VT<real>::N, vld<real>(W + v * VT<real>::N) + vld<real>(S + v * VT<real>::N));
+    const vec_t<real> s = vld<real>(S + v * VT<real>::N) + vsplat<real>(alpha) * vld<real>(P + v * VT<real>::N);
+    vst<real>(S + v * VT<real>::N, s);
+    vst<real>(W + v * VT<real>::N, vld<real>(W + v * VT<real>::N) + s);
   }
 }
 
 // ------------------------------------------------------- update rows ---
-// Per segment of row i: XS_i = X_i S; [first] P_i += XS_i;
-// y~_ij += <XS_i, q_j> for the segment's positives, both orientations
-// (update_cross, ffm.cpp:439-465).
+// Per segment of row i (one segment per subgroup): XS_i = X_i S;
+// [first] P_i += XS_i; base_ij += <XS_i, q_j> for the segment's positives, in
+// both orientations (update_cross, ffm.cpp:439-465).
 template <typename real, int KP>
 __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                             const int64_t *__restrict__ xptr,
@@ -716,15 +766,32 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
   using G = Geo<real, KP>;
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
-  for (uint64_t s = wave; s < nseg; s += nwaves) {
+  for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) {
     const Seg sgm = segs[s];
     const uint64_t i = sgm.row;
     vec_t<real> xs = vzero<real>();
-    for (int64_t p = xptr[i] + sg; p < xptr[i + 1]; p += G::NSG)
+    for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
       xs += vsplat<real>(xval[p]) * vld<real>(S + (size_t)xidx[p] * KP + li * G::VE);
-    xs = xsg_vsum<G::LPR, real>(xs);
-    if (sgm.first && sg == 0) vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
-    for (int64_t p = sgm.b + sg; p < sgm.e; p += G::NSG) {
+    if (seg_first(sgm)) vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
+    int64_t p = sgm.b;
+    for (; p + 3 < sgm.e; p += 4) {
+      const vec_t<real> q0 = vld<real>(Q1 + (size_t)ycol[p] * KP + li * G::VE);
+      const vec_t<real> q1 = vld<real>(Q1 + (size_t)ycol[p + 1] * KP + li * G::VE);
+      const vec_t<real> q2 = vld<real>(Q1 + (size_t)ycol[p + 2] * KP + li * G::VE);
+      const vec_t<real> q3 = vld<real>(Q1 + (size_t)ycol[p + 3] * KP + li * G::VE);
+      const real d0 = sg_sum<G::LPR>(hsum<real>(xs * q0));
+      const real d1 = sg_sum<G::LPR>(hsum<real>(xs * q1));
+      const real d2 = sg_sum<G::LPR>(hsum<real>(xs * q2));
+      const real d3 = sg_sum<G::LPR>(hsum<real>(xs * q3));
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+        if (u % G::LPR == li) {
+          const real d = u == 0 ? d0 : u == 1 ? d1 : u == 2 ? d2 : d3;
+          yt[p + u] += d;
+          yt_other[perm[p + u]] += d;
+        }
+    }
+    for (; p < sgm.e; p++) {
       const real d = sg_sum<G::LPR>(hsum<real>(xs * vld<real>(Q1 + (size_t)ycol[p] * KP + li * G::VE)));
       if (li == 0) {
         yt[p] += d;

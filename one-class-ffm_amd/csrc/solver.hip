@@ -144,6 +144,7 @@ template <typename real> struct DevField {
   DevBuf<real> scval;
   DevBuf<Chunk> schunks;
   DevBuf<unsigned> cnt;  // per-column arrival tickets of the fused feature pass (zero at rest)
+  bool idlike = false;   // one node per row and each feature in exactly one row (CSC = identity)
   // host copies kept until the segment CSC is built
   std::vector<int64_t> h_xptr;
   std::vector<uint32_t> h_xidx;
@@ -212,10 +213,11 @@ template <typename real> static void build_segments(DevSide<real> &s, const std:
   for (uint64_t i = 0; i < R; i++) {
     segptr[i] = (uint32_t)segs.size();
     const int64_t b = yptr[i], e = yptr[i + 1];
+    const uint32_t nrow = (uint32_t)std::max<int64_t>(1, (e - b + (int64_t)len - 1) / (int64_t)len);
     int64_t p = b;
     do {
       const int64_t q = std::min<int64_t>(e, p + (int64_t)len);
-      segs.push_back(Seg{(uint32_t)i, p == b ? 1u : 0u, p, q});
+      segs.push_back(Seg{(uint32_t)i, (nrow << 1) | (p == b ? 1u : 0u), p, q});
       p = q;
     } while (p < e);
   }
@@ -315,6 +317,7 @@ template <typename real> class Problem final : public ProblemBase {
     n_ = V.m;
     if (const char *e = std::getenv("OCFFM_SEG_LEN")) seg_len_ = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
     if (const char *e = std::getenv("OCFFM_LOOKAHEAD")) lookahead_ = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("OCFFM_FUSE")) no_fuse_ = std::atoi(e) == 0;  // id-field row fusion: opt-in
     // shard users contiguously
     u0_ = U.m * (uint64_t)comm_.rank / (uint64_t)comm_.nranks;
     u1_ = U.m * (uint64_t)(comm_.rank + 1) / (uint64_t)comm_.nranks;
@@ -700,6 +703,15 @@ template <typename real> class Problem final : public ProblemBase {
         xval.assign(d.xval[fi].begin() + base, d.xval[fi].begin() + d.xptr[fi][r1]);
       }
       F->nnz = xidx.size();
+      if (F->nnz == R && F->D == R && R > 0) {
+        std::vector<uint8_t> seen(F->D, 0);
+        bool ok = true;
+        for (uint64_t i = 0; i < R && ok; i++) {
+          if (xptr[i + 1] - xptr[i] != 1 || seen[xidx[xptr[i]]]) ok = false;
+          else seen[xidx[xptr[i]]] = 1;
+        }
+        F->idlike = ok;
+      }
       F->xptr.upload(xptr);
       F->xidx.upload(xidx);
       F->xval.upload(to_real(xval));
@@ -1076,6 +1088,7 @@ template <typename real> class Problem final : public ProblemBase {
   // gd_side / gd_cross (ffm.cpp:537-703) -> G, and the CG start vectors.
   void gradient(HalfCtx &h) {
     DevSide<real> &own = *h.own;
+    const bool fz_ = fused_rows(h);
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
       using Gm = Geo<real, KP>;
@@ -1088,17 +1101,24 @@ template <typename real> class Problem final : public ProblemBase {
         const bool lds = msz <= 64 * 1024;
         const double bytes = (double)own.R * 8 + (double)own.npos * (4 + rs) + (double)ps.R * KP * rs +
                              (double)C_ * own.R * KP * rs + (double)own.R * rs + (double)own.R * KP * rs;
-        prof_launch("gd_cross_row", bytes, [&] {
-          if (lds)
-            k_gd_cross_seg<real, KP, true><<<grid_for(own.nseg, 4), BLOCK, msz, stream_>>>(
-                own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
-                (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, h.partner->bias.p,
-                w_, r_, h_.p);
-          else
-            k_gd_cross_seg<real, KP, false><<<grid_for(own.nseg, 4), BLOCK, 0, stream_>>>(
-                own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
-                (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, h.partner->bias.p,
-                w_, r_, h_.p);
+        DevField<real> &F = *h.F;
+        const Fin<real> fin = make_fin(h, 0);
+        auto go = [&](auto fz, auto ml) {
+          constexpr bool FZ = decltype(fz)::value, ML = decltype(ml)::value;
+          k_gd_cross_seg<real, KP, ML, FZ><<<grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, ML ? msz : 0,
+                                            stream_>>>(
+              own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
+              (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, h.partner->bias.p, w_,
+              r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, fin);
+        };
+        prof_launch(fz_ ? "gd_cross_fused" : "gd_cross_row", bytes, [&] {
+          if (fz_) {
+            if (lds) go(std::true_type(), std::true_type());
+            else go(std::true_type(), std::false_type());
+          } else {
+            if (lds) go(std::false_type(), std::true_type());
+            else go(std::false_type(), std::false_type());
+          }
         });
         // QTQ for CG = M of this block
         const uint32_t c0 = cross_slot(std::min(h.fl, h.fo), std::max(h.fl, h.fo));
@@ -1110,15 +1130,43 @@ template <typename real> class Problem final : public ProblemBase {
         const double n1 = (double)other.R;
         const double bytes = (double)own.R * 8 + (double)own.npos * rs + (double)own.R * KP * rs * 2 +
                              (double)own.R * rs * 2;
-        prof_launch("gd_side_row", bytes, [&] {
-          k_gd_side_seg<real, KP><<<grid_for(own.nseg, 4), BLOCK, 0, stream_>>>(
-              own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, own.bias.p, other.bias.p, own.s.p,
-              sums_.p + 2 * KP, n1, w_, r_, h_.p);
+        DevField<real> &F = *h.F;
+        const Fin<real> fin = make_fin(h, 0);
+        auto go = [&](auto fz) {
+          constexpr bool FZ = decltype(fz)::value;
+          k_gd_side_seg<real, KP, FZ><<<grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, 0, stream_>>>(
+              own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, own.bias.p, other.bias.p, own.s.p, sums_.p + 2 * KP,
+              n1, w_, r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, fin);
+        };
+        prof_launch(fz_ ? "gd_side_fused" : "gd_side_row", bytes, [&] {
+          if (fz_) go(std::true_type());
+          else go(std::false_type());
         });
       }
-      feature_pass(h, 0, true);
+      if (!fz_) feature_pass(h, 0, true);
     });
   }
+
+  Fin<real> make_fin(const HalfCtx &h, int it) {
+    Fin<real> f;
+    f.fw = h.fw;
+    f.lam = lam_;
+    f.W = h.W1;
+    f.G = G_.p;
+    f.S = S_.p;
+    f.P = Vd_.p;
+    f.R = Rv_.p;
+    f.Hp = Hv_.p;
+    f.acc = acc_.p;
+    f.cnt = h.F->cnt.p;
+    f.st = st_.p;
+    f.part = part_.p;
+    f.run_host = run_host_dev_;
+    f.it = it;
+    return f;
+  }
+  // id-like field on one GPU: the row pass finalises its feature column.
+  bool fused_rows(const HalfCtx &h) const { return h.F->idlike && !comm_.active() && !no_fuse_; }
 
   // Feature pass of a half: fused gather + finalisation on one GPU; gather,
   // all-reduce, finalisation when the partial sums must meet across ranks.
@@ -1137,32 +1185,29 @@ template <typename real> class Problem final : public ProblemBase {
         const double bytes = (double)ent * (4 + rs) + (double)ent * KP * rs + (double)nch * sizeof(Chunk) +
                              (double)h.D * KP * rs * (it == 0 ? 6 : (it > 1 ? 4 : 2));
         const unsigned grid = grid_for(nch, 4 * Gm::NSG, 2048);
+        const Fin<real> fin = make_fin(h, it);
         if (it == 0)
           prof_launch("feat_grad", bytes, [&] {
-            k_feat<real, KP, 0><<<grid, BLOCK, 0, stream_>>>(
-                0, nch, seg ? F.schunks.p : F.chunks.p, seg ? F.scrow.p : F.crow.p, seg ? F.scval.p : F.cval.p, h_.p,
-                acc_.p, F.cnt.p, h.fw, lam_, h.W1, G_.p, S_.p, Vd_.p, Rv_.p, Hv_.p, st_.p, part_.p, run_host_dev_);
+            k_feat<real, KP, 0><<<grid, BLOCK, 0, stream_>>>(nch, seg ? F.schunks.p : F.chunks.p,
+                                                            seg ? F.scrow.p : F.crow.p, seg ? F.scval.p : F.cval.p,
+                                                            h_.p, fin);
           });
         else
           prof_launch("feat_hv", bytes, [&] {
-            k_feat<real, KP, 1><<<grid, BLOCK, 0, stream_>>>(
-                it, nch, seg ? F.schunks.p : F.chunks.p, seg ? F.scrow.p : F.crow.p, seg ? F.scval.p : F.cval.p,
-                h_.p, acc_.p, F.cnt.p, h.fw, lam_, h.W1, G_.p, S_.p, Vd_.p, Rv_.p, Hv_.p, st_.p, part_.p,
-                run_host_dev_);
+            k_feat<real, KP, 1><<<grid, BLOCK, 0, stream_>>>(nch, seg ? F.schunks.p : F.chunks.p,
+                                                            seg ? F.scrow.p : F.crow.p, seg ? F.scval.p : F.cval.p,
+                                                            h_.p, fin);
           });
         return;
       }
       scatter(F, run, seg);
+      const Fin<real> fin = make_fin(h, it);
+      const unsigned grid = grid_for(nv, BLOCK, 2048);
       if (it == 0)
-        prof_launch("grad_fin", (double)h.D * KP * rs * 7, [&] {
-          k_grad_fin<real, KP><<<grid_for(nv, BLOCK, 2048), BLOCK, 0, stream_>>>(
-              nv, h.W1, h.fw, lam_, acc_.p, G_.p, Rv_.p, Vd_.p, S_.p, st_.p, part_.p, run_host_dev_);
-        });
+        prof_launch("grad_fin", (double)h.D * KP * rs * 6, [&] { k_fin<real, KP, 0><<<grid, BLOCK, 0, stream_>>>(nv, fin); });
       else
-        prof_launch("hv_fin", (double)h.D * KP * rs * 4, [&] {
-          k_hv_fin<real, KP><<<grid_for(nv, BLOCK, 2048), BLOCK, 0, stream_>>>(it, nv, h.fw, lam_, acc_.p, Vd_.p,
-                                                                              Rv_.p, Hv_.p, st_.p, part_.p);
-        });
+        prof_launch("hv_fin", (double)h.D * KP * rs * (it > 1 ? 11 : 5),
+                    [&] { k_fin<real, KP, 1><<<grid, BLOCK, 0, stream_>>>(nv, fin); });
     });
   }
 
@@ -1170,59 +1215,65 @@ template <typename real> class Problem final : public ProblemBase {
   void hv_pass(HalfCtx &h, int it) {
     DevSide<real> &own = *h.own;
     const int *run = &st_.p->run[it];
+    const bool fz_ = fused_rows(h);
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
       using Gm = Geo<real, KP>;
       const double rs = sizeof(real);
       DevField<real> &F = *h.F;
+      const Fin<real> fin = make_fin(h, it);
       if (own.R) {
         if (h.cross) {
           const size_t qsz = (size_t)KP * KP * sizeof(real);
           const bool lds = qsz <= 32 * 1024;
-          const size_t smem = (lds ? qsz : 0) + 4 * KP * sizeof(real);
+          const size_t smem = (lds ? qsz : 0) + (size_t)(BLOCK / Gm::LPR) * KP * sizeof(real);
           const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
                                (double)own.npos * 4 + (double)h.partner->R * KP * rs + (double)own.R * KP * rs;
-          prof_launch("hs_cross_row", bytes, [&] {
-            if (lds)
-              k_hs_cross_seg<real, KP, true><<<grid_for(own.nseg, 4), BLOCK, smem, stream_>>>(
-                  own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.ycol.p, h.Q1, QTQ_.p, w_, h_.p,
-                  run, Rv_.p, st_.p, it);
-            else
-              k_hs_cross_seg<real, KP, false><<<grid_for(own.nseg, 4), BLOCK, smem, stream_>>>(
-                  own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.ycol.p, h.Q1, QTQ_.p, w_, h_.p,
-                  run, Rv_.p, st_.p, it);
+          auto go = [&](auto fz, auto ml) {
+            constexpr bool FZ = decltype(fz)::value, ML = decltype(ml)::value;
+            k_hs_cross_seg<real, KP, ML, FZ><<<grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, smem,
+                                              stream_>>>(own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p,
+                                                         own.ycol.p, h.Q1, QTQ_.p, w_, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
+                                                         fin);
+          };
+          prof_launch(fz_ ? "hs_cross_fused" : "hs_cross_row", bytes, [&] {
+            if (fz_) {
+              if (lds) go(std::true_type(), std::true_type());
+              else go(std::true_type(), std::false_type());
+            } else {
+              if (lds) go(std::false_type(), std::true_type());
+              else go(std::false_type(), std::false_type());
+            }
           });
         } else {
           DevSide<real> &other = h.user ? V_ : U_;
           const double n1 = (double)other.R;
           const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
                                (double)own.R * KP * rs * 2;
-          prof_launch("hs_side_row", bytes, [&] {
-            k_hs_side_row<real, KP><<<grid_for(own.R, 4 * Gm::NSG), BLOCK, 0, stream_>>>(
-                own.R, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.yptr.p, h.Q1, w_, n1, h_.p, run, Rv_.p, st_.p, it);
+          auto go = [&](auto fz) {
+            constexpr bool FZ = decltype(fz)::value;
+            k_hs_side_row<real, KP, FZ><<<grid_for(own.R, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, 0, stream_>>>(
+                own.R, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.yptr.p, h.Q1, w_, n1, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
+                fin);
+          };
+          prof_launch(fz_ ? "hs_side_fused" : "hs_side_row", bytes, [&] {
+            if (fz_) go(std::true_type());
+            else go(std::false_type());
           });
         }
       }
     });
-    feature_pass(h, it, h.cross);
-  }
-
-  void cg_tail(HalfCtx &h, int it) {
-    with_kp(kp_, [&](auto K) {
-      constexpr int KP = decltype(K)::value;
-      using Gm = Geo<real, KP>;
-      const uint64_t nv = h.D * KP / Gm::VE;
-      const double rs = sizeof(real);
-      prof_launch("cg_update", (double)h.D * KP * rs * 6, [&] {
-        k_cg_upd<real, KP><<<grid_for(nv, BLOCK, 2048), BLOCK, 0, stream_>>>(it, nv, Vd_.p, Hv_.p, S_.p, Rv_.p,
-                                                                            st_.p, part_.p, run_host_dev_);
-      });
-    });
+    if (!fz_) feature_pass(h, it, h.cross);
   }
 
   // One half of a block: gradient, Newton-CG, update (ffm.cpp:826-832, 843-849).
   void half(uint32_t f1, uint32_t f2, int which) {
     HalfCtx h = half_ctx(f1, f2, which);
+    hipEvent_t hb = nullptr;
+    if (profiling && prof_filter.empty()) {
+      hb = ev();
+      HIPCHK(hipEventRecord(hb, stream_));
+    }
     gradient(h);
     // CG with `lookahead_` iterations in flight (see file header): iteration
     // it is enqueued before the host waits for iteration it-L's verdict, so
@@ -1240,7 +1291,6 @@ template <typename real> class Problem final : public ProblemBase {
     };
     for (int it = 1; it <= MAXCG && !done; it++) {
       hv_pass(h, it);
-      cg_tail(h, it);
       hipEvent_t e = ev();
       HIPCHK(hipEventRecord(e, stream_));
       evs.push_back(e);
@@ -1262,8 +1312,8 @@ template <typename real> class Problem final : public ProblemBase {
       using Gm = Geo<real, KP>;
       const double rs = sizeof(real);
       const uint64_t nv = h.D * KP / Gm::VE;
-      prof_launch("apply_step", (double)h.D * KP * rs * 3, [&] {
-        k_axpy1<real><<<grid_for(nv, BLOCK, 2048), BLOCK, 0, stream_>>>(nv, S_.p, h.W1);
+      prof_launch("apply_step", (double)h.D * KP * rs * 5, [&] {
+        k_apply<real><<<grid_for(nv, BLOCK, 2048), BLOCK, 0, stream_>>>(nv, Vd_.p, S_.p, h.W1, st_.p);
       });
       if (own.R == 0) return;
       DevField<real> &F = *h.F;
@@ -1273,7 +1323,7 @@ template <typename real> class Problem final : public ProblemBase {
                              (double)own.R * KP * rs * 2 + (double)own.npos * (4 + 4 + 4 * rs) +
                              (double)other.R * KP * rs;
         prof_launch("update_cross_row", bytes, [&] {
-          k_update_cross_seg<real, KP><<<grid_for(own.nseg, 4), BLOCK, 0, stream_>>>(
+          k_update_cross_seg<real, KP><<<grid_for(own.nseg, 4 * Gm::NSG), BLOCK, 0, stream_>>>(
               own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, own.ycol.p, own.yt.p, other.yt.p,
               own.perm.p, h.Q1);
         });
@@ -1289,6 +1339,13 @@ template <typename real> class Problem final : public ProblemBase {
     });
     cg_log.push_back(nr);
     account_half(h, nr);
+    if (hb) {
+      hipEvent_t he = ev();
+      HIPCHK(hipEventRecord(he, stream_));
+      char name[32];
+      std::snprintf(name, sizeof(name), "half(%u,%u)%c", f1, f2, which ? 'H' : 'W');
+      pending_.push_back({name, 0.0, hb, he});
+    }
   }
 
   // Algorithmic bytes of one half (SURVEY §8d formula, s = sizeof(real)).
@@ -1321,8 +1378,9 @@ template <typename real> class Problem final : public ProblemBase {
   uint32_t k_, kp_, fu_, fv_, f_, C_ = 0;
   double w_, lam_, r_;
   uint64_t m_glob_ = 0, n_ = 0, u0_ = 0, u1_ = 0, dmax_ = 0, npop_ = 0;
-  uint64_t seg_len_ = 128;
+  uint64_t seg_len_ = 32;
   int lookahead_ = 1;
+  bool no_fuse_ = true;
   DevSide<real> U_, V_, T_;
   std::vector<Block> blocks_;
   std::vector<DevBuf<real>> W_, H_, P_, Q_;

@@ -174,6 +174,20 @@ def test_kkbox_small_fp64(kk_small):
     np.testing.assert_allclose(vg["prec"], vo["prec"], atol=1e-12)
 
 
+@pytest.mark.parametrize("env", [{"OCFFM_FUSE": "1"}, {"OCFFM_SEG_LEN": "3"}, {"OCFFM_LOOKAHEAD": "3"},
+                                 {"OCFFM_FUSE": "1", "OCFFM_SEG_LEN": "2"}])
+def test_execution_variants_fp64(kk_small, monkeypatch, env):
+    """Schedule knobs (id-field row fusion, segment length, CG look-ahead)
+    change the kernels that run, never the result."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    o, g = pair(kk_small, with_test=False)
+    o.one_epoch()
+    g.one_epoch()
+    assert_state(o, g, 1e-9)
+    np.testing.assert_array_equal(g.cg_log(), o.cg_log())
+
+
 def test_cold_rows_and_duplicate_labels():
     ds = synth.tiny(seed=6)
     # a test row whose features are all dropped -> popularity scores

@@ -19,6 +19,7 @@ The JSON line also carries:
                  fp64) timed on this host on a bounded sample, rank 0, N=1.
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -46,7 +47,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--precision", choices=["fp32", "fp64"], default="fp32")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    ap.add_argument("--cpu-epochs", type=int, default=1)
+    ap.add_argument("--cpu-epochs", type=int, default=4)
     return ap.parse_args()
 
 
@@ -80,7 +81,8 @@ def main():
     for _ in range(max(1, args.warmup)):
         g.one_epoch()
     ks = g.kernel_stats()
-    dominant = max(ks.items(), key=lambda kv: kv[1]["total_ms"])[0]
+    dominant = max(((k, v) for k, v in ks.items() if not k.startswith("half(")),
+                   key=lambda kv: kv[1]["total_ms"])[0]
     g.reset_stats()
     g.set_profile_filter(dominant)
 
@@ -112,8 +114,10 @@ def main():
             "epoch_alg_bytes": alg / max(1, args.steps)}
     # HBM bytes per launch of the same kernel family from the committed
     # rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, MI355X guide §HBM).
-    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
+    pmcs = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json")))
+    if pmcs:
+        pmc = pmcs[-1]
+        roof["traffic_source"] = os.path.relpath(pmc, REPO)
         try:
             t = json.load(open(pmc)).get(dominant)
             roof["traffic"] = None if t is None else round(t["bytes_per_launch"])

@@ -18,10 +18,11 @@ from collections import defaultdict
 FAMILY = [
     ("k_hs_cross_seg", "hs_cross_row"), ("k_hs_side_row", "hs_side_row"), ("k_feat<float, 32, 1>", "feat_hv"),
     ("k_feat<double, 32, 1>", "feat_hv"), ("k_feat<float, 32, 0>", "feat_grad"), ("k_feat<double, 32, 0>", "feat_grad"),
-    ("k_cg_upd", "cg_update"), ("k_gd_cross_seg", "gd_cross_row"), ("k_gd_side_seg", "gd_side_row"),
-    ("k_update_cross_seg", "update_cross_row"), ("k_update_side_seg", "update_side_row"),
-    ("k_gram_part", "aggregates"), ("k_reduce_parts", "aggr_reduce"), ("k_axpy1", "apply_step"),
-    ("k_rowdot_multi", "rowdot_multi"), ("k_csc", "csc_scatter"), ("k_hv_fin", "hv_fin"), ("k_grad_fin", "grad_fin"),
+("k_gd_cross_seg", "gd_cross_row"), ("k_gd_side_seg", "gd_side_row"),
+    ("k_update_cross_seg", "update_cross_row"), ("k_update_side_row", "update_side_row"),
+    ("k_gram_part", "aggregates"), ("k_reduce_parts", "aggr_reduce"), ("k_apply", "apply_step"),
+    ("k_rowdot_multi", "rowdot_multi"), ("k_csc", "csc_scatter"), ("k_fin<float, 32, 1>", "hv_fin"),
+    ("k_fin<double, 32, 1>", "hv_fin"), ("k_fin<float, 32, 0>", "grad_fin"), ("k_fin<double, 32, 0>", "grad_fin"),
 ]
 
 

@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace ocffm {
 
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -49,11 +51,22 @@ constexpr int BLOCK = 256;   // 4 waves
 constexpr int MAXCG = 20;    // ffm.cpp:761
 constexpr double CG_EPS = 9e-2;  // ffm.cpp:762
 
-struct Chunk {  // a run of CSC entries of one feature column
-  uint32_t col;
-  uint32_t nch;  // chunks of this column (1: this chunk owns the column)
+// One subgroup's share of a feature pass over the feature-major (CSC) view
+// of a field.  A column with <= JOB_ENT entries is one "light" job, finished
+// by its subgroup.  A heavier column is cut into wave-chunks of NSG jobs
+// (one wave, JOB_ENT entries per subgroup) summed across the wave; a column
+// of several wave-chunks is summed by the last chunk to arrive, from the
+// partial slots in chunk order (deterministic, no float atomics).
+// Every subgroup issues its JOB_ENT row loads at once: one latency round.
+struct Job {
+  uint32_t col;     // JOB_NONE: padding
+  uint32_t nparts;  // wave-chunks of the column (wave jobs), else 1
+  uint32_t slot;    // wave jobs: partial slot of this wave-chunk
+  uint32_t flags;   // bit 0: wave job; bits 1..: wave-chunk index in the column
   int64_t b, e;
 };
+constexpr uint32_t JOB_NONE = 0xffffffffu;
+constexpr int JOB_ENT = 8;
 
 // A run of one row's positives [b, e): rows with many positives (popular
 // items: the Pareto head holds ~all users) are split so that no wave walks
@@ -102,12 +115,128 @@ template <typename real> __device__ __forceinline__ vec_t<real> vsplat(real x) {
   return v;
 }
 
+// ------------------------------------------------------ lane exchange ---
+// DPP lane moves run on the VALU (no LDS-pipe ds_bpermute).  Controls:
+// quad_perm 0x00-0xff, row_shl:n 0x100+n, row_shr:n 0x110+n,
+// row_mirror 0x140, row_half_mirror 0x141.
+template <int CTRL> __device__ __forceinline__ uint32_t dpp32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+struct W2 {
+  uint32_t lo, hi;
+};
+template <int CTRL, typename T> __device__ __forceinline__ T dpp(T x) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "dpp: 32/64-bit values");
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, dpp32<CTRL>(__builtin_bit_cast(uint32_t, x)));
+  } else {
+    W2 w = __builtin_bit_cast(W2, x);
+    w.lo = dpp32<CTRL>(w.lo);
+    w.hi = dpp32<CTRL>(w.hi);
+    return __builtin_bit_cast(T, w);
+  }
+}
+
 // Sum over the LPR lanes of one subgroup (all of them active together).
+// Every lane ends with the same bits (each step adds a commuted pair).
 template <int LPR, typename T> __device__ __forceinline__ T sg_sum(T x) {
-#pragma unroll
-  for (int o = LPR / 2; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  if constexpr (LPR >= 2) x += dpp<0xB1>(x);   // quad_perm [1,0,3,2]: xor 1
+  if constexpr (LPR >= 4) x += dpp<0x4E>(x);   // quad_perm [2,3,0,1]: xor 2
+  if constexpr (LPR >= 8) x += dpp<0x141>(x);  // half-row mirror: the other quad
+  if constexpr (LPR >= 16) x += dpp<0x140>(x); // row mirror: the other half-row
+  if constexpr (LPR >= 32) x += __shfl_xor(x, 16, 64);
+  if constexpr (LPR >= 64) x += __shfl_xor(x, 32, 64);
   return x;
 }
+
+// Value of lane SRC of the caller's LPR-lane subgroup, in every lane of it.
+template <int LPR, int SRC, typename T> __device__ __forceinline__ T sg_bcast(T x, int li) {
+  if constexpr (LPR == 1) {
+    return x;
+  } else if constexpr (LPR == 2) {
+    return dpp<(SRC | SRC << 2 | (2 + SRC) << 4 | (2 + SRC) << 6)>(x);
+  } else if constexpr (LPR == 4) {
+    return dpp<SRC * 0x55>(x);
+  } else if constexpr (LPR == 8) {
+    const T a = dpp<(SRC % 4) * 0x55>(x);  // lane SRC%4 of each quad
+    if constexpr (SRC < 4) {
+      const T b = dpp<0x114>(a);  // row_shr:4: the upper quad takes the lower one's
+      return (li & 4) ? b : a;
+    } else {
+      const T b = dpp<0x104>(a);  // row_shl:4: the lower quad takes the upper one's
+      return (li & 4) ? a : b;
+    }
+  } else {
+    return __shfl(x, (int)((threadIdx.x & 63) & ~(LPR - 1)) + SRC, 64);
+  }
+}
+
+template <int... I> struct iseq {};
+template <int N, int... I> struct make_iseq : make_iseq<N - 1, N - 1, I...> {};
+template <int... I> struct make_iseq<0, I...> {
+  using type = iseq<I...>;
+};
+template <typename F, int... I> __device__ __forceinline__ void sfor_impl(F &&f, iseq<I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+// Compile-time unrolled loop: f(integral_constant<int, 0..N-1>).
+template <int N, typename F> __device__ __forceinline__ void sfor(F &&f) {
+  sfor_impl(f, typename make_iseq<N>::type{});
+}
+
+// Raw-buffer view of a table for gathers.  A load at an out-of-range offset
+// returns zero without a memory access (the buffer range check), so the
+// unused slots of a fixed-width gather need neither a branch nor a wait:
+// all of a subgroup's loads go out in one round.  Tables < 4 GiB (host-checked).
+struct BufView {
+  __amdgpu_buffer_rsrc_t r;
+  uint32_t oob;  // an offset past the end
+};
+__device__ __forceinline__ BufView buf_view(const void *p, uint64_t bytes) {
+  return BufView{__builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)(uint32_t)bytes, 0x00020000),
+                 (uint32_t)bytes};
+}
+template <typename real> __device__ __forceinline__ vec_t<real> bld(const BufView &b, uint32_t off) {
+  return __builtin_bit_cast(vec_t<real>, __builtin_amdgcn_raw_buffer_load_b128(b.r, off, 0, 0));
+}
+template <typename real> __device__ __forceinline__ real bld1(const BufView &b, uint32_t off);
+template <> __device__ __forceinline__ float bld1<float>(const BufView &b, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(b.r, off, 0, 0));
+}
+template <> __device__ __forceinline__ double bld1<double>(const BufView &b, uint32_t off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(b.r, off, 0, 0));
+}
+
+// A pass over up to PW positions [p0, p0+PW) of a positive segment, spread
+// over the LPR lanes of the subgroup: lane li holds the column (ycol) of
+// positions p0 + li + t*LPR, t < UT, loaded in one round; position `pos`
+// of the pass is then read from lane pos % LPR, slot pos / LPR.  Gathers of
+// partner rows go out GB at a time through a BufView (absent positions load
+// zero rows), so a 32-position segment costs 1 + 32/GB latency rounds
+// instead of one per position.
+constexpr uint32_t POS_NONE = 0xffffffffu;
+template <typename real, int KP, int GB_ = 8> struct PosPass {
+  using G = Geo<real, KP>;
+  static constexpr int PW = G::LPR > 32 ? G::LPR : 32;
+  static constexpr int UT = PW / G::LPR;
+  static constexpr int GB = GB_ < PW ? GB_ : PW;  // gathers per round
+  static constexpr uint32_t ROWB = KP * sizeof(real);
+  template <int POS, typename T> static __device__ __forceinline__ T at(const T (&v)[UT], int li) {
+    return sg_bcast<G::LPR, POS % G::LPR>(v[POS / G::LPR], li);
+  }
+  static __device__ __forceinline__ void load_cols(const uint32_t *__restrict__ ycol, int64_t p0, int64_t e, int li,
+                                                   uint32_t (&jj)[UT]) {
+#pragma unroll
+    for (int t = 0; t < UT; t++) {
+      const int64_t q = p0 + li + t * G::LPR;
+      jj[t] = q < e ? ycol[q] : POS_NONE;
+    }
+  }
+  static __device__ __forceinline__ uint32_t row_off(uint32_t j, const BufView &b, int li) {
+    return j == POS_NONE ? b.oob : j * ROWB + (uint32_t)li * 16u;
+  }
+};
+
 // Sum over the NSG subgroups of a wave (lane-wise, whole wave active).
 template <int LPR, typename T> __device__ __forceinline__ T xsg_sum(T x) {
 #pragma unroll
@@ -160,13 +289,30 @@ __device__ __forceinline__ bool last_block(const double (&v)[NV], double *part, 
   }
   __syncthreads();
   if (!s_last) return false;
+  // All partials in one round: sc1 buffer loads (aux 16), out-of-range
+  // slots read zero; fixed summation order (thread, then round, then tree).
+  const BufView pv = buf_view(part, (uint64_t)gridDim.x * NV * sizeof(double));
+  double x[NV];
 #pragma unroll
-  for (int k = 0; k < NV; k++) {
-    double x = 0;
-    for (unsigned b = threadIdx.x; b < gridDim.x; b += BLOCK)
-      x += __hip_atomic_load(&part[(size_t)b * NV + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    tot[k] = block_sum(x);
+  for (int k = 0; k < NV; k++) x[k] = 0;
+  constexpr int ROUND = 8;  // blocks per thread per round
+  for (unsigned b0 = 0; b0 < gridDim.x; b0 += ROUND * BLOCK) {
+    double y[ROUND][NV];
+#pragma unroll
+    for (int u = 0; u < ROUND; u++)
+#pragma unroll
+      for (int k = 0; k < NV; k++) {
+        const unsigned b = b0 + u * BLOCK + threadIdx.x;
+        y[u][k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                 pv.r, b < gridDim.x ? (b * NV + k) * 8u : pv.oob, 0, 16));
+      }
+#pragma unroll
+    for (int u = 0; u < ROUND; u++)
+#pragma unroll
+      for (int k = 0; k < NV; k++) x[k] += y[u][k];
   }
+#pragma unroll
+  for (int k = 0; k < NV; k++) tot[k] = block_sum(x[k]);
   if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
 }
@@ -236,14 +382,37 @@ __device__ __forceinline__ bool col_arrive(const Fin<real> &f, uint32_t col, uns
 // MODE 1 (Hessian-vector, ffm.cpp:783-809): apply iteration it-1's update
 //   (S += a p, r -= a Hp, p = r + b p), then Hp = lam f p + s;
 //   ds += (<p,Hp>, <r,Hp>, |Hp|^2).
+// The operands a column's finalisation reads (fin_load) do not depend on
+// the column sum, so a kernel can issue them before its gather.
+template <typename real> struct FinOps {
+  vec_t<real> w_or_p, r, hp, s;
+  real reg;
+};
 template <typename real, int KP, int MODE>
-__device__ __forceinline__ void col_finalize(const Fin<real> &f, uint32_t col, vec_t<real> s, real alpha, real beta,
-                                             bool upd, int li, double (&ds)[3]) {
+__device__ __forceinline__ FinOps<real> fin_load(const Fin<real> &f, uint32_t col, bool upd, int li) {
   using G = Geo<real, KP>;
   const size_t off = (size_t)col * KP + li * G::VE;
-  const real reg = (real)(f.fw ? f.lam * (double)f.fw[col] : f.lam);
+  FinOps<real> o;
+  o.reg = (real)(f.fw ? f.lam * (double)f.fw[col] : f.lam);
   if (MODE == 0) {
-    const vec_t<real> g = vsplat<real>(reg) * vld<real>(f.W + off) + s;
+    o.w_or_p = vld<real>(f.W + off);
+  } else {
+    o.w_or_p = vld<real>(f.P + off);
+    o.r = vld<real>(f.R + off);
+    if (upd) {
+      o.hp = vld<real>(f.Hp + off);
+      o.s = vld<real>(f.S + off);
+    }
+  }
+  return o;
+}
+template <typename real, int KP, int MODE>
+__device__ __forceinline__ void col_finalize(const Fin<real> &f, uint32_t col, vec_t<real> s, real alpha, real beta,
+                                             bool upd, int li, double (&ds)[3], const FinOps<real> &o) {
+  using G = Geo<real, KP>;
+  const size_t off = (size_t)col * KP + li * G::VE;
+  if (MODE == 0) {
+    const vec_t<real> g = vsplat<real>(o.reg) * o.w_or_p + s;
     if (f.G) vst<real>(f.G + off, g);
     vst<real>(f.R + off, -g);
     vst<real>(f.P + off, -g);
@@ -251,19 +420,15 @@ __device__ __forceinline__ void col_finalize(const Fin<real> &f, uint32_t col, v
 #pragma unroll
     for (int e = 0; e < G::VE; e++) ds[0] += (double)g[e] * (double)g[e];
   } else {
-    vec_t<real> rn, pe;
+    vec_t<real> rn = o.r, pe = o.w_or_p;
     if (upd) {
-      const vec_t<real> po = vld<real>(f.P + off);
-      rn = vld<real>(f.R + off) - vsplat<real>(alpha) * vld<real>(f.Hp + off);
-      pe = rn + vsplat<real>(beta) * po;
-      vst<real>(f.S + off, vld<real>(f.S + off) + vsplat<real>(alpha) * po);
+      rn = o.r - vsplat<real>(alpha) * o.hp;
+      pe = rn + vsplat<real>(beta) * o.w_or_p;
+      vst<real>(f.S + off, o.s + vsplat<real>(alpha) * o.w_or_p);
       vst<real>(f.R + off, rn);
       vst<real>(f.P + off, pe);
-    } else {
-      rn = vld<real>(f.R + off);
-      pe = vld<real>(f.P + off);
     }
-    const vec_t<real> hp = vsplat<real>(reg) * pe + s;
+    const vec_t<real> hp = vsplat<real>(o.reg) * pe + s;
     vst<real>(f.Hp + off, hp);
 #pragma unroll
     for (int e = 0; e < G::VE; e++) {
@@ -272,6 +437,11 @@ __device__ __forceinline__ void col_finalize(const Fin<real> &f, uint32_t col, v
       ds[2] += (double)hp[e] * (double)hp[e];
     }
   }
+}
+template <typename real, int KP, int MODE>
+__device__ __forceinline__ void col_finalize(const Fin<real> &f, uint32_t col, vec_t<real> s, real alpha, real beta,
+                                             bool upd, int li, double (&ds)[3]) {
+  col_finalize<real, KP, MODE>(f, col, s, alpha, beta, upd, li, ds, fin_load<real, KP, MODE>(f, col, upd, li));
 }
 
 // Grid-wide end of a finalising kernel.  MODE 0 publishes g2 and the first
@@ -416,8 +586,11 @@ __global__ __launch_bounds__(BLOCK) void k_gd_cross_seg(uint64_t nseg, const Seg
                                                         double w, double r, real *__restrict__ h,
                                                         const int64_t *__restrict__ xptr,
                                                         const uint32_t *__restrict__ xidx,
-                                                        const real *__restrict__ xval, Fin<real> f) {
+                                                        const real *__restrict__ xval, uint64_t q1rows,
+                                                        Fin<real> f) {
   using G = Geo<real, KP>;
+  using PP = PosPass<real, KP>;
+  const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real)), bb = buf_view(b1, q1rows * sizeof(real));
   extern __shared__ __align__(16) unsigned char smem_raw[];
   real *Ms = reinterpret_cast<real *>(smem_raw);
   const real *Mp = M;
@@ -442,21 +615,30 @@ __global__ __launch_bounds__(BLOCK) void k_gd_cross_seg(uint64_t nseg, const Seg
     const uint64_t i = sgm.row;
     const real ai = a1[i];
     vec_t<real> pk = vzero<real>();
-    int64_t p = sgm.b;
-    for (; p + 3 < sgm.e; p += 4) {
-      const uint32_t j0 = ycol[p], j1 = ycol[p + 1], j2 = ycol[p + 2], j3 = ycol[p + 3];
-      const vec_t<real> q0 = vld<real>(Q1 + (size_t)j0 * KP + li * G::VE);
-      const vec_t<real> q1 = vld<real>(Q1 + (size_t)j1 * KP + li * G::VE);
-      const vec_t<real> q2 = vld<real>(Q1 + (size_t)j2 * KP + li * G::VE);
-      const vec_t<real> q3 = vld<real>(Q1 + (size_t)j3 * KP + li * G::VE);
-      pk += vsplat<real>(cpos * (yt[p] + ai + b1[j0]) - cneg) * q0;
-      pk += vsplat<real>(cpos * (yt[p + 1] + ai + b1[j1]) - cneg) * q1;
-      pk += vsplat<real>(cpos * (yt[p + 2] + ai + b1[j2]) - cneg) * q2;
-      pk += vsplat<real>(cpos * (yt[p + 3] + ai + b1[j3]) - cneg) * q3;
-    }
-    for (; p < sgm.e; p++) {
-      const uint32_t j0 = ycol[p];
-      pk += vsplat<real>(cpos * (yt[p] + ai + b1[j0]) - cneg) * vld<real>(Q1 + (size_t)j0 * KP + li * G::VE);
+    for (int64_t p0 = sgm.b; p0 < sgm.e; p0 += PP::PW) {
+      uint32_t jj[PP::UT];
+      real yv[PP::UT];
+      PP::load_cols(ycol, p0, sgm.e, li, jj);
+#pragma unroll
+      for (int t = 0; t < PP::UT; t++) {
+        const int64_t q = p0 + li + t * G::LPR;
+        yv[t] = q < sgm.e ? yt[q] : (real)0;
+      }
+      sfor<PP::PW / PP::GB>([&](auto BT) {
+        constexpr int bt = decltype(BT)::value * PP::GB;
+        if (p0 + bt >= sgm.e) return;
+        vec_t<real> qv[PP::GB];
+        real cb[PP::GB], yb[PP::GB];
+        sfor<PP::GB>([&](auto U) {
+          constexpr int u = decltype(U)::value;
+          const uint32_t j = PP::template at<bt + u>(jj, li);
+          yb[u] = PP::template at<bt + u>(yv, li);
+          qv[u] = bld<real>(qb, PP::row_off(j, qb, li));
+          cb[u] = bld1<real>(bb, j == POS_NONE ? bb.oob : j * (uint32_t)sizeof(real));
+        });
+#pragma unroll
+        for (int u = 0; u < PP::GB; u++) pk += vsplat<real>(cpos * (yb[u] + ai + cb[u]) - cneg) * qv[u];
+      });
     }
     if (seg_first(sgm)) {
       vec_t<real> t = vzero<real>();
@@ -492,8 +674,10 @@ __global__ __launch_bounds__(BLOCK) void k_gd_side_seg(uint64_t nseg, const Seg 
                                                        double r, real *__restrict__ h,
                                                        const int64_t *__restrict__ xptr,
                                                        const uint32_t *__restrict__ xidx,
-                                                       const real *__restrict__ xval, Fin<real> f) {
+                                                       const real *__restrict__ xval, uint64_t nb1, Fin<real> f) {
   using G = Geo<real, KP>;
+  using PP = PosPass<real, KP>;
+  const BufView bb = buf_view(b1, nb1 * sizeof(real));
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
   const real cpos = (real)(1 - w), cneg = (real)(w * (1 - r));
@@ -504,7 +688,20 @@ __global__ __launch_bounds__(BLOCK) void k_gd_side_seg(uint64_t nseg, const Seg 
     const uint64_t i = sgm.row;
     const real ai = a1[i];
     real z = 0;
-    for (int64_t p = sgm.b + li; p < sgm.e; p += G::LPR) z += cpos * (yt[p] + ai + b1[ycol[p]]) - cneg;
+    for (int64_t p0 = sgm.b; p0 < sgm.e; p0 += PP::PW) {
+      uint32_t jj[PP::UT];
+      real yv[PP::UT], cb[PP::UT];
+      PP::load_cols(ycol, p0, sgm.e, li, jj);
+#pragma unroll
+      for (int t = 0; t < PP::UT; t++) {
+        const int64_t q = p0 + li + t * G::LPR;
+        yv[t] = q < sgm.e ? yt[q] : (real)0;
+        cb[t] = bld1<real>(bb, jj[t] == POS_NONE ? bb.oob : jj[t] * (uint32_t)sizeof(real));
+      }
+#pragma unroll
+      for (int t = 0; t < PP::UT; t++)
+        if (p0 + li + t * G::LPR < sgm.e) z += cpos * (yv[t] + ai + cb[t]) - cneg;
+    }
     z = sg_sum<G::LPR>(z);
     if (seg_first(sgm)) z += (real)(w * (n1 * ((double)ai - r) + bs + (double)sa1[i]));
     vec_t<real> out = vsplat<real>(z) * vld<real>(Q1 + i * KP + li * G::VE);
@@ -567,11 +764,14 @@ __global__ __launch_bounds__(BLOCK) void k_hs_cross_seg(uint64_t nseg, const Seg
                                                         const uint32_t *__restrict__ xidx,
                                                         const real *__restrict__ xval, const real *__restrict__ V,
                                                         const uint32_t *__restrict__ ycol,
-                                                        const real *__restrict__ Q1, const real *__restrict__ QTQ,
-                                                        double w, real *__restrict__ h, const int *__restrict__ run,
-                                                        const real *__restrict__ Rv, const real *__restrict__ Hv,
-                                                        const CgState *st, int it, Fin<real> f) {
+                                                        const real *__restrict__ Q1, uint64_t q1rows,
+                                                        const real *__restrict__ QTQ, double w, real *__restrict__ h,
+                                                        const int *__restrict__ run, const real *__restrict__ Rv,
+                                                        const real *__restrict__ Hv, const CgState *st, int it,
+                                                        Fin<real> f) {
   using G = Geo<real, KP>;
+  using PP = PosPass<real, KP, 32>;  // 32 gathers in flight per subgroup: latency-bound
+  const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real));
   if (run && !*run) return;
   const bool upd = st && it > 1;
   const real alpha = upd ? (real)st->alpha : (real)0, beta = upd ? (real)st->beta : (real)0;
@@ -596,25 +796,23 @@ __global__ __launch_bounds__(BLOCK) void k_hs_cross_seg(uint64_t nseg, const Seg
     for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
       phi += vsplat<real>(xval[p]) * cg_dir_at<real, KP>(V, Rv, Hv, alpha, beta, upd, (size_t)xidx[p] * KP + li * G::VE);
     vec_t<real> ka = vzero<real>();
-    int64_t p = sgm.b;
-    for (; p + 3 < sgm.e; p += 4) {
-      const uint32_t j0 = ycol[p], j1 = ycol[p + 1], j2 = ycol[p + 2], j3 = ycol[p + 3];
-      const vec_t<real> q0 = vld<real>(Q1 + (size_t)j0 * KP + li * G::VE);
-      const vec_t<real> q1 = vld<real>(Q1 + (size_t)j1 * KP + li * G::VE);
-      const vec_t<real> q2 = vld<real>(Q1 + (size_t)j2 * KP + li * G::VE);
-      const vec_t<real> q3 = vld<real>(Q1 + (size_t)j3 * KP + li * G::VE);
-      const real s0 = sg_sum<G::LPR>(hsum<real>(phi * q0));
-      const real s1 = sg_sum<G::LPR>(hsum<real>(phi * q1));
-      const real s2 = sg_sum<G::LPR>(hsum<real>(phi * q2));
-      const real s3 = sg_sum<G::LPR>(hsum<real>(phi * q3));
-      ka += vsplat<real>(s0) * q0;
-      ka += vsplat<real>(s1) * q1;
-      ka += vsplat<real>(s2) * q2;
-      ka += vsplat<real>(s3) * q3;
-    }
-    for (; p < sgm.e; p++) {
-      const vec_t<real> q0 = vld<real>(Q1 + (size_t)ycol[p] * KP + li * G::VE);
-      ka += vsplat<real>(sg_sum<G::LPR>(hsum<real>(phi * q0))) * q0;
+    for (int64_t p0 = sgm.b; p0 < sgm.e; p0 += PP::PW) {
+      uint32_t jj[PP::UT];
+      PP::load_cols(ycol, p0, sgm.e, li, jj);
+      sfor<PP::PW / PP::GB>([&](auto BT) {
+        constexpr int bt = decltype(BT)::value * PP::GB;
+        if (p0 + bt >= sgm.e) return;
+        vec_t<real> qv[PP::GB];
+        sfor<PP::GB>([&](auto U) {
+          constexpr int u = decltype(U)::value;
+          qv[u] = bld<real>(qb, PP::row_off(PP::template at<bt + u>(jj, li), qb, li));
+        });
+        real dv[PP::GB];
+#pragma unroll
+        for (int u = 0; u < PP::GB; u++) dv[u] = sg_sum<G::LPR>(hsum<real>(phi * qv[u]));
+#pragma unroll
+        for (int u = 0; u < PP::GB; u++) ka += vsplat<real>(dv[u]) * qv[u];
+      });
     }
     vec_t<real> out = vsplat<real>(cpos) * ka;
     if (seg_first(sgm)) {
@@ -638,79 +836,91 @@ __global__ __launch_bounds__(BLOCK) void k_hs_cross_seg(uint64_t nseg, const Seg
   if (FUSE) fin_blocks<real, 1>(f, dsum);
 }
 
-// ---------------------------------------------------------- CSC scatter ---
-// acc[col] (+)= sum_{(r,val) in chunk} val * h[r].  For segment-mode passes
-// the CSC is built over segments (r = segment id), so a popular row's
-// partials are spread over many chunks instead of one serial sum.
-// One chunk per subgroup; single-chunk columns store, others add atomically.
-template <typename real, int KP>
-__global__ __launch_bounds__(BLOCK) void k_csc(uint64_t nch, const Chunk *__restrict__ ch,
-                                               const uint32_t *__restrict__ crow, const real *__restrict__ cval,
-                                               const real *__restrict__ h, real *__restrict__ acc,
-                                               const int *__restrict__ run) {
-  using G = Geo<real, KP>;
-  if (run && !*run) return;
-  WAVE_SETUP
-  const int sg = lane / G::LPR, li = lane % G::LPR;
-  for (uint64_t c = wave * G::NSG + sg; c < nch; c += nwaves * G::NSG) {
-    const Chunk k = ch[c];
-    vec_t<real> s = vzero<real>();
-    int64_t p = k.b;
-    for (; p + 3 < k.e; p += 4) {
-      const uint32_t r0 = crow[p], r1 = crow[p + 1], r2 = crow[p + 2], r3 = crow[p + 3];
-      const vec_t<real> h0 = vld<real>(h + (size_t)r0 * KP + li * G::VE);
-      const vec_t<real> h1 = vld<real>(h + (size_t)r1 * KP + li * G::VE);
-      const vec_t<real> h2 = vld<real>(h + (size_t)r2 * KP + li * G::VE);
-      const vec_t<real> h3 = vld<real>(h + (size_t)r3 * KP + li * G::VE);
-      s += vsplat<real>(cval[p]) * h0;
-      s += vsplat<real>(cval[p + 1]) * h1;
-      s += vsplat<real>(cval[p + 2]) * h2;
-      s += vsplat<real>(cval[p + 3]) * h3;
-    }
-    for (; p < k.e; p++) s += vsplat<real>(cval[p]) * vld<real>(h + (size_t)crow[p] * KP + li * G::VE);
-    real *dst = acc + (size_t)k.col * KP + li * G::VE;
-    if (k.nch == 1) {
-      vst<real>(dst, s);
-    } else {
-#pragma unroll
-      for (int e = 0; e < G::VE; e++) unsafeAtomicAdd(dst + e, s[e]);
-    }
-  }
-}
-
-// Fused feature pass (single GPU): CSC gather of h per column chunk, then the
-// column's finalisation by its only chunk or by the last of its chunks
-// (col_arrive / col_finalize above).
+// ------------------------------------------------------ feature pass ---
+// acc_col = sum_{(r, x) in column} x h[r] for every feature column of a field
+// (the X^T h of gd_* / hs_*, ffm.cpp:561-570, 603-624, 715-742), then
+// MODE 0: gradient finalisation, MODE 1: Hessian-vector finalisation of CG
+// iteration f.it (col_finalize above), MODE 2: store the column sums into
+// f.acc (multi-GPU: the all-reduce and k_fin follow).
 template <typename real, int KP, int MODE>
-__global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nch, const Chunk *__restrict__ ch,
+__global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__restrict__ jobs,
                                                 const uint32_t *__restrict__ crow, const real *__restrict__ cval,
-                                                const real *__restrict__ h, Fin<real> f) {
+                                                const real *__restrict__ h, uint64_t hbytes, real *__restrict__ wpart,
+                                                Fin<real> f) {
   using G = Geo<real, KP>;
-  if (MODE == 1 && !f.st->run[f.it]) return;
+  if (f.it > 0 && !f.st->run[f.it]) return;
+  const BufView hb = buf_view(h, hbytes);
   const bool upd = MODE == 1 && f.it > 1;
   const real alpha = upd ? (real)f.st->alpha : (real)0, beta = upd ? (real)f.st->beta : (real)0;
-  WAVE_SETUP
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
   const int sg = lane / G::LPR, li = lane % G::LPR;
   double dsum[3] = {0, 0, 0};
-  for (uint64_t c = wave * G::NSG + sg; c < nch; c += nwaves * G::NSG) {
-    const Chunk k = ch[c];
-    vec_t<real> s = vzero<real>();
-    int64_t p = k.b;
-    for (; p + 3 < k.e; p += 4) {
-      const uint32_t r0 = crow[p], r1 = crow[p + 1], r2 = crow[p + 2], r3 = crow[p + 3];
-      const vec_t<real> h0 = vld<real>(h + (size_t)r0 * KP + li * G::VE);
-      const vec_t<real> h1 = vld<real>(h + (size_t)r1 * KP + li * G::VE);
-      const vec_t<real> h2 = vld<real>(h + (size_t)r2 * KP + li * G::VE);
-      const vec_t<real> h3 = vld<real>(h + (size_t)r3 * KP + li * G::VE);
-      s += vsplat<real>(cval[p]) * h0;
-      s += vsplat<real>(cval[p + 1]) * h1;
-      s += vsplat<real>(cval[p + 2]) * h2;
-      s += vsplat<real>(cval[p + 3]) * h3;
+  if (wave < nwave) {
+    const Job jb = jobs[wave * G::NSG + sg];
+    // finalisation operands first (padding jobs read column 0, unused)
+    FinOps<real> ops;
+    if (MODE != 2) ops = fin_load<real, KP, (MODE == 2 ? 0 : MODE)>(f, jb.col == JOB_NONE ? 0u : jb.col, upd, li);
+    constexpr int U = (JOB_ENT + G::LPR - 1) / G::LPR;
+    uint32_t rr[U];
+    real vv[U];
+#pragma unroll
+    for (int t = 0; t < U; t++) {
+      const int e = li + t * G::LPR;
+      const bool ok = e < JOB_ENT && jb.b + e < jb.e;
+      rr[t] = ok ? crow[jb.b + e] : 0u;
+      vv[t] = ok ? cval[jb.b + e] : (real)0;
     }
-    for (; p < k.e; p++) s += vsplat<real>(cval[p]) * vld<real>(h + (size_t)crow[p] * KP + li * G::VE);
-    if (col_arrive<real, KP>(f, k.col, k.nch, s, sg, li)) col_finalize<real, KP, MODE>(f, k.col, s, alpha, beta, upd, li, dsum);
+    vec_t<real> hv[JOB_ENT];
+#pragma unroll
+    for (int e = 0; e < JOB_ENT; e++) {
+      const uint32_t r = __shfl(rr[e / G::LPR], sg * G::LPR + e % G::LPR, 64);
+      const real x = __shfl(vv[e / G::LPR], sg * G::LPR + e % G::LPR, 64);
+      const uint32_t off = jb.b + e < jb.e ? r * (uint32_t)(KP * sizeof(real)) + li * 16u : hb.oob;
+      hv[e] = vsplat<real>(x) * bld<real>(hb, off);
+    }
+    vec_t<real> s = hv[0];
+#pragma unroll
+    for (int e = 1; e < JOB_ENT; e++) s += hv[e];
+    bool mine = jb.col != JOB_NONE;
+    if (jb.flags & 1u) {  // wave job (wave-uniform)
+      s = xsg_vsum<G::LPR, real>(s);
+      mine = sg == 0;
+      if (jb.nparts > 1) {
+        if (sg == 0) {
+#pragma unroll
+          for (int e = 0; e < G::VE; e++)
+            __hip_atomic_store(wpart + (size_t)jb.slot * KP + li * G::VE + e, s[e], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned t = 0;
+        if (lane == 0) t = __hip_atomic_fetch_add(f.cnt + jb.col, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = __shfl(t, 0, 64);
+        if (t != jb.nparts - 1) {
+          mine = false;
+        } else {
+          const uint32_t s0 = jb.slot - (jb.flags >> 1);
+          vec_t<real> a = vzero<real>();
+          for (uint32_t q = sg; q < jb.nparts; q += G::NSG) {
+            vec_t<real> x;
+#pragma unroll
+            for (int e = 0; e < G::VE; e++)
+              x[e] = __hip_atomic_load(wpart + (size_t)(s0 + q) * KP + li * G::VE + e, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            a += x;
+          }
+          s = xsg_vsum<G::LPR, real>(a);
+          if (lane == 0) __hip_atomic_store(f.cnt + jb.col, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    if (mine) {
+      if (MODE == 2) vst<real>(f.acc + (size_t)jb.col * KP + li * G::VE, s);
+      else col_finalize<real, KP, (MODE == 2 ? 0 : MODE)>(f, jb.col, s, alpha, beta, upd, li, dsum, ops);
+    }
   }
-  fin_blocks<real, MODE>(f, dsum);
+  if (MODE != 2) fin_blocks<real, (MODE == 2 ? 0 : MODE)>(f, dsum);
 }
 
 // ------------------------------------------------- CG vector kernels ---
@@ -762,8 +972,10 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
                                                             const uint32_t *__restrict__ ycol,
                                                             real *__restrict__ yt, real *__restrict__ yt_other,
                                                             const uint32_t *__restrict__ perm,
-                                                            const real *__restrict__ Q1) {
+                                                            const real *__restrict__ Q1, uint64_t q1rows) {
   using G = Geo<real, KP>;
+  using PP = PosPass<real, KP>;
+  const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real));
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
   for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) {
@@ -773,29 +985,43 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
     for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
       xs += vsplat<real>(xval[p]) * vld<real>(S + (size_t)xidx[p] * KP + li * G::VE);
     if (seg_first(sgm)) vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
-    int64_t p = sgm.b;
-    for (; p + 3 < sgm.e; p += 4) {
-      const vec_t<real> q0 = vld<real>(Q1 + (size_t)ycol[p] * KP + li * G::VE);
-      const vec_t<real> q1 = vld<real>(Q1 + (size_t)ycol[p + 1] * KP + li * G::VE);
-      const vec_t<real> q2 = vld<real>(Q1 + (size_t)ycol[p + 2] * KP + li * G::VE);
-      const vec_t<real> q3 = vld<real>(Q1 + (size_t)ycol[p + 3] * KP + li * G::VE);
-      const real d0 = sg_sum<G::LPR>(hsum<real>(xs * q0));
-      const real d1 = sg_sum<G::LPR>(hsum<real>(xs * q1));
-      const real d2 = sg_sum<G::LPR>(hsum<real>(xs * q2));
-      const real d3 = sg_sum<G::LPR>(hsum<real>(xs * q3));
+    for (int64_t p0 = sgm.b; p0 < sgm.e; p0 += PP::PW) {
+      uint32_t jj[PP::UT], pp[PP::UT];
+      PP::load_cols(ycol, p0, sgm.e, li, jj);
+      PP::load_cols(perm, p0, sgm.e, li, pp);
+      real dd[PP::UT];
 #pragma unroll
-      for (int u = 0; u < 4; u++)
-        if (u % G::LPR == li) {
-          const real d = u == 0 ? d0 : u == 1 ? d1 : u == 2 ? d2 : d3;
-          yt[p + u] += d;
-          yt_other[perm[p + u]] += d;
+      for (int t = 0; t < PP::UT; t++) dd[t] = 0;
+      sfor<PP::PW / PP::GB>([&](auto BT) {
+        constexpr int bt = decltype(BT)::value * PP::GB;
+        if (p0 + bt >= sgm.e) return;
+        vec_t<real> qv[PP::GB];
+        sfor<PP::GB>([&](auto U) {
+          constexpr int u = decltype(U)::value;
+          qv[u] = bld<real>(qb, PP::row_off(PP::template at<bt + u>(jj, li), qb, li));
+        });
+#pragma unroll
+        for (int u = 0; u < PP::GB; u++) {
+          const real d = sg_sum<G::LPR>(hsum<real>(xs * qv[u]));
+          if ((bt + u) % G::LPR == li) dd[(bt + u) / G::LPR] = d;
         }
-    }
-    for (; p < sgm.e; p++) {
-      const real d = sg_sum<G::LPR>(hsum<real>(xs * vld<real>(Q1 + (size_t)ycol[p] * KP + li * G::VE)));
-      if (li == 0) {
-        yt[p] += d;
-        yt_other[perm[p]] += d;
+      });
+      // each lane owns its positions p0 + li + t*LPR: all loads, then all stores
+      // (distinct positives: the scattered targets never alias)
+      real yo[PP::UT], ym[PP::UT];
+#pragma unroll
+      for (int t = 0; t < PP::UT; t++) {
+        const int64_t q = p0 + li + t * G::LPR;
+        ym[t] = q < sgm.e ? yt[q] : (real)0;
+        yo[t] = q < sgm.e ? yt_other[pp[t]] : (real)0;
+      }
+#pragma unroll
+      for (int t = 0; t < PP::UT; t++) {
+        const int64_t q = p0 + li + t * G::LPR;
+        if (q < sgm.e) {
+          yt[q] = ym[t] + dd[t];
+          yt_other[pp[t]] = yo[t] + dd[t];
+        }
       }
     }
   }

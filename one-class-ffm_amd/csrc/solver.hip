@@ -95,6 +95,7 @@ template <typename T> struct DevBuf {
     if (count) HIPCHK(hipMemcpy(p, src, count * sizeof(T), hipMemcpyHostToDevice));
   }
   void upload(const std::vector<T> &v) { upload(v.data(), v.size()); }
+  uint64_t bytes() const { return (uint64_t)n * sizeof(T); }
 };
 
 static uint32_t block_index(uint32_t f1, uint32_t f2, uint32_t f) { return f2 + (f - 1) * f1 - f1 * (f1 - 1) / 2; }
@@ -138,13 +139,15 @@ template <typename real> struct DevField {
   DevBuf<real> xval;
   DevBuf<uint32_t> crow;
   DevBuf<real> cval;
-  DevBuf<Chunk> chunks;
+  DevBuf<Job> jobs;  // kernels.hpp: Job; njw waves of NSG jobs
+  uint64_t njw = 0, nslot = 0;
   DevBuf<real> freqw;  // global feature frequency (for --freq)
   // the same CSC over positive segments (kernels.hpp: Seg) of the side
   DevBuf<uint32_t> scrow;
   DevBuf<real> scval;
-  DevBuf<Chunk> schunks;
-  DevBuf<unsigned> cnt;  // per-column arrival tickets of the fused feature pass (zero at rest)
+  DevBuf<Job> sjobs;
+  uint64_t snjw = 0, snslot = 0;
+  DevBuf<unsigned> cnt;  // per-column arrival tickets (zero at rest)
   bool idlike = false;   // one node per row and each feature in exactly one row (CSC = identity)
   // host copies kept until the segment CSC is built
   std::vector<int64_t> h_xptr;
@@ -172,7 +175,7 @@ template <typename real> struct DevSide {
 
 // Split every row's positives into segments of at most `len` (rows without
 // positives still get one, empty, segment for their row-local terms).
-template <typename real> static void build_seg_csc(DevSide<real> &s, const std::vector<uint32_t> &segptr) {
+template <typename real> static void build_seg_csc(DevSide<real> &s, const std::vector<uint32_t> &segptr, int nsg) {
   for (auto &Fp : s.F) {
     DevField<real> &F = *Fp;
     const uint64_t R = F.h_xptr.size() - 1;
@@ -191,12 +194,13 @@ template <typename real> static void build_seg_csc(DevSide<real> &s, const std::
       }
     std::vector<uint32_t> crow;
     std::vector<double> cval;
-    std::vector<Chunk> ch;
-    build_csc(sidx, F.D, xptr.data(), xidx.data(), xval.data(), crow, cval, ch);
+    std::vector<Job> jobs;
+    build_csc(sidx, F.D, xptr.data(), xidx.data(), xval.data(), nsg, crow, cval, jobs, F.snslot);
     F.scrow.upload(crow);
     std::vector<real> cv(cval.begin(), cval.end());
     F.scval.upload(cv);
-    F.schunks.upload(ch);
+    F.sjobs.upload(jobs);
+    F.snjw = jobs.size() / nsg;
     F.h_xptr.clear();
     F.h_xptr.shrink_to_fit();
     F.h_xidx.clear();
@@ -206,7 +210,8 @@ template <typename real> static void build_seg_csc(DevSide<real> &s, const std::
   }
 }
 
-template <typename real> static void build_segments(DevSide<real> &s, const std::vector<int64_t> &yptr, uint64_t len) {
+template <typename real>
+static void build_segments(DevSide<real> &s, const std::vector<int64_t> &yptr, uint64_t len, int nsg) {
   const uint64_t R = yptr.size() - 1;
   std::vector<Seg> segs;
   std::vector<uint32_t> segptr(R + 1, 0);
@@ -226,7 +231,7 @@ template <typename real> static void build_segments(DevSide<real> &s, const std:
   s.nseg = segs.size();
   s.segs.upload(segs);
   s.segptr.upload(segptr);
-  build_seg_csc(s, segptr);
+  build_seg_csc(s, segptr, nsg);
 }
 
 struct Block {
@@ -234,9 +239,13 @@ struct Block {
   uint32_t f1 = 0, f2 = 0;
 };
 
-// CSC with chunks (feature-major view of one field's CSR) built on the host.
-static void build_csc(uint64_t R, uint64_t D, const int64_t *xptr, const uint32_t *xidx, const double *xval,
-                      std::vector<uint32_t> &crow, std::vector<double> &cval, std::vector<Chunk> &chunks) {
+// Feature-major (CSC) view of one field's CSR and its feature-pass jobs
+// (kernels.hpp: Job): light columns first, packed NSG to a wave, then the
+// wave-chunks of the heavy columns.  Empty columns get a job too (their
+// finalisation is lam W alone).
+static void build_csc(uint64_t R, uint64_t D, const int64_t *xptr, const uint32_t *xidx, const double *xval, int nsg,
+                      std::vector<uint32_t> &crow, std::vector<double> &cval, std::vector<Job> &jobs,
+                      uint64_t &nslot) {
   const uint64_t nnz = (uint64_t)xptr[R] - (uint64_t)xptr[0];
   std::vector<uint64_t> cptr(D + 1, 0);
   for (int64_t p = xptr[0]; p < xptr[R]; p++) cptr[xidx[p] + 1]++;
@@ -250,17 +259,24 @@ static void build_csc(uint64_t R, uint64_t D, const int64_t *xptr, const uint32_
       crow[q] = (uint32_t)i;
       cval[q] = xval[p];
     }
-  // chunk length: keep every subgroup's sequential sum short.
-  const uint64_t CH = 32;
-  chunks.clear();
+  jobs.clear();
+  for (uint64_t d = 0; d < D; d++)
+    if (cptr[d + 1] - cptr[d] <= (uint64_t)JOB_ENT)
+      jobs.push_back(Job{(uint32_t)d, 1u, 0u, 0u, (int64_t)cptr[d], (int64_t)cptr[d + 1]});
+  while (jobs.size() % nsg) jobs.push_back(Job{JOB_NONE, 1u, 0u, 0u, 0, 0});
+  const uint64_t wc = (uint64_t)nsg * JOB_ENT;
+  nslot = 0;
   for (uint64_t d = 0; d < D; d++) {
     const uint64_t b = cptr[d], e = cptr[d + 1];
-    if (e - b <= CH) {
-      chunks.push_back(Chunk{(uint32_t)d, 1u, (int64_t)b, (int64_t)e});
-    } else {
-      const uint32_t nc = (uint32_t)((e - b + CH - 1) / CH);
-      for (uint64_t s = b; s < e; s += CH) chunks.push_back(Chunk{(uint32_t)d, nc, (int64_t)s, (int64_t)std::min(e, s + CH)});
-    }
+    if (e - b <= (uint64_t)JOB_ENT) continue;
+    const uint32_t np = (uint32_t)((e - b + wc - 1) / wc);
+    for (uint32_t q = 0; q < np; q++)
+      for (int g = 0; g < nsg; g++) {
+        const int64_t sb = (int64_t)std::min(e, b + q * wc + (uint64_t)g * JOB_ENT);
+        const int64_t se = (int64_t)std::min<uint64_t>(e, (uint64_t)sb + JOB_ENT);
+        jobs.push_back(Job{(uint32_t)d, np, (uint32_t)(nslot + q), 1u | (q << 1), sb, se});
+      }
+    nslot += np;
   }
 }
 
@@ -352,6 +368,14 @@ template <typename real> class Problem final : public ProblemBase {
     Rv_.alloc(dk);
     Hv_.alloc(dk);
     h_.alloc(std::max<uint64_t>(std::max(Rmax, std::max(U_.nseg, V_.nseg)), 1) * kp_);
+    if (std::max(U_.R, V_.R) * kp_ * sizeof(real) >= (1ull << 32) - 64)  // partner-row gathers (BufView)
+      throw Error(OCFFM_E_DATA, "too many rows per GPU for 32-bit gather offsets; shard over more GPUs");
+    if (h_.bytes() >= (1ull << 32) - 64)  // kernels.hpp: BufView gathers use 32-bit offsets
+      throw Error(OCFFM_E_DATA, "too many rows/segments per GPU for one partial buffer; shard over more GPUs");
+    uint64_t nslot = 1;
+    for (DevSide<real> *sd : {&U_, &V_})
+      for (auto &F : sd->F) nslot = std::max(nslot, std::max(F->nslot, F->snslot));
+    wpart_.alloc(nslot * kp_);
     C_ = fu_ * fv_;
     M_.alloc(std::max<uint32_t>(C_, 1) * kp_ * kp_);
     QTQ_.alloc((size_t)kp_ * kp_);
@@ -718,11 +742,12 @@ template <typename real> class Problem final : public ProblemBase {
       F->xval.upload(to_real(xval));
       std::vector<uint32_t> crow;
       std::vector<double> cval;
-      std::vector<Chunk> ch;
-      build_csc(R, F->D, xptr.data(), xidx.data(), xval.data(), crow, cval, ch);
+      std::vector<Job> jobs;
+      build_csc(R, F->D, xptr.data(), xidx.data(), xval.data(), nsg(), crow, cval, jobs, F->nslot);
       F->crow.upload(crow);
       F->cval.upload(to_real(cval));
-      F->chunks.upload(ch);
+      F->jobs.upload(jobs);
+      F->njw = jobs.size() / nsg();
       F->cnt.alloc(std::max<uint64_t>(F->D, 1));
       F->h_xptr = std::move(xptr);
       F->h_xidx = std::move(xidx);
@@ -747,7 +772,7 @@ template <typename real> class Problem final : public ProblemBase {
     std::vector<uint32_t> ycol(pe - pb);
     for (uint64_t p = pb; p < pe; p++) ycol[p - pb] = (uint32_t)U.ycol[p];
     U_.npos = pe - pb;
-    build_segments(U_, yptr, seg_len_);
+    build_segments(U_, yptr, seg_len_, nsg());
     U_.yptr.upload(yptr);
     U_.ycol.upload(ycol);
     U_.yt.alloc(std::max<uint64_t>(U_.npos, 1));
@@ -779,7 +804,7 @@ template <typename real> class Problem final : public ProblemBase {
         v2u[q] = (uint32_t)(p - pb);
       }
     V_.npos = np;
-    build_segments(V_, vptr, seg_len_);
+    build_segments(V_, vptr, seg_len_, nsg());
     V_.yptr.upload(vptr);
     V_.ycol.upload(vcol);
     V_.yt.alloc(std::max<uint64_t>(np, 1));
@@ -1016,25 +1041,6 @@ template <typename real> class Problem final : public ProblemBase {
 
   // CSC scatter of h into acc over one field, then the all-reduce (if any).
   // seg: h holds per-segment partials (use the segment CSC of the field).
-  void scatter(DevField<real> &F, const int *run, bool seg) {
-    const uint64_t nch = seg ? F.schunks.n : F.chunks.n;
-    if (nch) {
-      with_kp(kp_, [&](auto K) {
-        constexpr int KP = decltype(K)::value;
-        using Gm = Geo<real, KP>;
-        const uint64_t ent = seg ? F.scrow.n : F.crow.n;
-        const double bytes = (double)ent * (4 + sizeof(real)) + (double)ent * kp_ * sizeof(real) +
-                             (double)F.D * kp_ * sizeof(real) + (double)nch * sizeof(Chunk);
-        prof_launch("csc_scatter", bytes, [&] {
-          launch(k_csc<real, KP>, grid_for(nch, 4 * Gm::NSG), BLOCK, 0,
-              nch, seg ? F.schunks.p : F.chunks.p, seg ? F.scrow.p : F.crow.p, seg ? F.scval.p : F.cval.p, h_.p,
-              acc_.p, run);
-        });
-      });
-    }
-    allreduce_dev(acc_.p, F.D * kp_);
-  }
-
   void allreduce_dev(real *buf, uint64_t count) {
     if (!comm_.active()) return;
     if (comm_.nccl) {
@@ -1127,7 +1133,7 @@ template <typename real> class Problem final : public ProblemBase {
           launch(k_gd_cross_seg<real, KP, ML, FZ>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, ML ? msz : 0,
               own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
               (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, h.partner->bias.p, w_,
-              r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, fin);
+              r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, (uint64_t)h.partner->R, fin);
         };
         prof_launch(fz_ ? "gd_cross_fused" : "gd_cross_row", bytes, [&] {
           if (fz_) {
@@ -1154,7 +1160,7 @@ template <typename real> class Problem final : public ProblemBase {
           constexpr bool FZ = decltype(fz)::value;
           launch(k_gd_side_seg<real, KP, FZ>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, 0,
               own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, own.bias.p, other.bias.p, own.s.p, sums_.p + 2 * KP,
-              n1, w_, r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, fin);
+              n1, w_, r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, (uint64_t)other.R, fin);
         };
         prof_launch(fz_ ? "gd_side_fused" : "gd_side_row", bytes, [&] {
           if (fz_) go(std::true_type());
@@ -1164,6 +1170,9 @@ template <typename real> class Problem final : public ProblemBase {
       if (!fz_) feature_pass(h, 0, true);
     });
   }
+
+  // subgroups per wave of this problem's row geometry (kernels.hpp: Geo)
+  int nsg() const { return 64 / std::max<int>(1, (int)(kp_ * sizeof(real) / 16)); }
 
   Fin<real> make_fin(const HalfCtx &h, int it) {
     Fin<real> f;
@@ -1186,45 +1195,61 @@ template <typename real> class Problem final : public ProblemBase {
   // id-like field on one GPU: the row pass finalises its feature column.
   bool fused_rows(const HalfCtx &h) const { return h.F->idlike && !comm_.active() && !no_fuse_; }
 
+  void scatter(HalfCtx &h, int it, bool seg) {
+    DevField<real> &F = *h.F;
+    feat_launch(h, it, seg, 2);
+    allreduce_dev(acc_.p, F.D * kp_);
+  }
+
+  // One feature pass (kernels.hpp: k_feat) over the row or segment CSC of
+  // the half's field.  mode 0/1 finalise (gradient / Hessian-vector of CG
+  // iteration it); mode 2 stores the column sums into acc_.
+  void feat_launch(HalfCtx &h, int it, bool seg, int mode) {
+    DevField<real> &F = *h.F;
+    const uint64_t njw = seg ? F.snjw : F.njw;
+    if (!njw) return;
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      using Gm = Geo<real, KP>;
+      const double rs = sizeof(real);
+      const uint64_t ent = seg ? F.scrow.n : F.crow.n;
+      const double vecs = mode == 2 ? 1 : (mode == 0 ? 5 : (it > 1 ? 8 : 3));
+      const double bytes = (double)ent * (4 + rs) + (double)ent * KP * rs + (double)njw * Gm::NSG * sizeof(Job) +
+                           (double)h.D * KP * rs * vecs;
+      const unsigned grid = (unsigned)((njw + 3) / 4);
+      const Fin<real> fin = make_fin(h, it);
+      const Job *jobs = seg ? F.sjobs.p : F.jobs.p;
+      const uint32_t *crow = seg ? F.scrow.p : F.crow.p;
+      const real *cval = seg ? F.scval.p : F.cval.p;
+      const char *name = mode == 2 ? "csc_scatter" : (mode == 0 ? "feat_grad" : "feat_hv");
+      prof_launch(name, bytes, [&] {
+        if (mode == 0) launch(k_feat<real, KP, 0>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, fin);
+        else if (mode == 1) launch(k_feat<real, KP, 1>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, fin);
+        else launch(k_feat<real, KP, 2>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, fin);
+      });
+    });
+  }
+
   // Feature pass of a half: fused gather + finalisation on one GPU; gather,
   // all-reduce, finalisation when the partial sums must meet across ranks.
   // mode 0: gradient (it = 0), mode 1: Hessian-vector of CG iteration `it`.
   void feature_pass(HalfCtx &h, int it, bool seg) {
-    DevField<real> &F = *h.F;
-    const int *run = it > 0 ? &st_.p->run[it] : nullptr;
+    if (!comm_.active()) {
+      feat_launch(h, it, seg, it == 0 ? 0 : 1);
+      return;
+    }
+    scatter(h, it, seg);
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
       using Gm = Geo<real, KP>;
       const double rs = sizeof(real);
       const uint64_t nv = h.D * KP / Gm::VE;
-      if (!comm_.active()) {
-        const uint64_t nch = seg ? F.schunks.n : F.chunks.n;
-        const uint64_t ent = seg ? F.scrow.n : F.crow.n;
-        const double bytes = (double)ent * (4 + rs) + (double)ent * KP * rs + (double)nch * sizeof(Chunk) +
-                             (double)h.D * KP * rs * (it == 0 ? 6 : (it > 1 ? 4 : 2));
-        const unsigned grid = grid_for(nch, 4 * Gm::NSG, 2048);
-        const Fin<real> fin = make_fin(h, it);
-        if (it == 0)
-          prof_launch("feat_grad", bytes, [&] {
-            launch(k_feat<real, KP, 0>, grid, BLOCK, 0, nch, seg ? F.schunks.p : F.chunks.p,
-                                                            seg ? F.scrow.p : F.crow.p, seg ? F.scval.p : F.cval.p,
-                                                            h_.p, fin);
-          });
-        else
-          prof_launch("feat_hv", bytes, [&] {
-            launch(k_feat<real, KP, 1>, grid, BLOCK, 0, nch, seg ? F.schunks.p : F.chunks.p,
-                                                            seg ? F.scrow.p : F.crow.p, seg ? F.scval.p : F.cval.p,
-                                                            h_.p, fin);
-          });
-        return;
-      }
-      scatter(F, run, seg);
       const Fin<real> fin = make_fin(h, it);
       const unsigned grid = grid_for(nv, BLOCK, 2048);
       if (it == 0)
         prof_launch("grad_fin", (double)h.D * KP * rs * 6, [&] { launch(k_fin<real, KP, 0>, grid, BLOCK, 0, nv, fin); });
       else
-        prof_launch("hv_fin", (double)h.D * KP * rs * (it > 1 ? 11 : 5),
+        prof_launch("hv_fin", (double)h.D * KP * rs * (it > 1 ? 9 : 4),
                     [&] { launch(k_fin<real, KP, 1>, grid, BLOCK, 0, nv, fin); });
     });
   }
@@ -1250,7 +1275,7 @@ template <typename real> class Problem final : public ProblemBase {
           auto go = [&](auto fz, auto ml) {
             constexpr bool FZ = decltype(fz)::value, ML = decltype(ml)::value;
             launch(k_hs_cross_seg<real, KP, ML, FZ>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, smem, own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p,
-                                                         own.ycol.p, h.Q1, QTQ_.p, w_, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
+                                                         own.ycol.p, h.Q1, (uint64_t)h.partner->R, QTQ_.p, w_, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
                                                          fin);
           };
           prof_launch(fz_ ? "hs_cross_fused" : "hs_cross_row", bytes, [&] {
@@ -1342,7 +1367,7 @@ template <typename real> class Problem final : public ProblemBase {
         prof_launch("update_cross_row", bytes, [&] {
           launch(k_update_cross_seg<real, KP>, grid_for(own.nseg, 4 * Gm::NSG), BLOCK, 0,
               own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, own.ycol.p, own.yt.p, other.yt.p,
-              own.perm.p, h.Q1);
+              own.perm.p, h.Q1, (uint64_t)other.R);
         });
       } else {
         DevSide<real> &other = h.user ? V_ : U_;
@@ -1403,7 +1428,7 @@ template <typename real> class Problem final : public ProblemBase {
   DevSide<real> U_, V_, T_;
   std::vector<Block> blocks_;
   std::vector<DevBuf<real>> W_, H_, P_, Q_;
-  DevBuf<real> acc_, G_, S_, Vd_, Rv_, Hv_, h_, M_, QTQ_;
+  DevBuf<real> acc_, G_, S_, Vd_, Rv_, Hv_, h_, M_, QTQ_, wpart_;
   DevBuf<double> sums_, vecs_, part_, at_d_, popular_;
   DevBuf<uint8_t> cold_;
   DevBuf<CgState> st_;

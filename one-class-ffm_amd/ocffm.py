@@ -19,7 +19,7 @@ except Exception:  # pragma: no cover - torch is optional for the library itself
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libocffm.so")
+LIB_PATH = os.environ.get("OCFFM_LIB") or os.path.join(HERE, "libocffm.so")  # override: experiment builds
 
 OK, E_ARG, E_IO, E_DATA, E_HIP, E_COMM, E_STATE = range(7)
 FP64, FP32 = 64, 32

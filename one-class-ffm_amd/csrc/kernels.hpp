@@ -66,7 +66,7 @@ struct Job {
   int64_t b, e;
 };
 constexpr uint32_t JOB_NONE = 0xffffffffu;
-constexpr int JOB_ENT = 8;
+constexpr int JOB_ENT = 8;  // entries per job (JE) of fields with multi-entry columns; unit fields use 1
 
 // A run of one row's positives [b, e): rows with many positives (popular
 // items: the Pareto head holds ~all users) are split so that no wave walks
@@ -86,7 +86,6 @@ struct CgState {
   double g2, r2, alpha, beta, vhv;
   int run[MAXCG + 2];  // run[it]: CG iteration `it` (1-based) executes
   int nr_cg;
-  unsigned counter;    // last-block ticket of the reductions below
   double scal[4];      // misc scalars (sum of a partner bias, ...)
 };
 
@@ -275,17 +274,34 @@ __device__ __forceinline__ double block_sum(double v) {
 // block; the block whose add returns gridDim-1 reads every partial with sc1
 // loads after a workgroup barrier.  No L2 write-back fence is needed.
 // Partials are summed in block order: deterministic for a fixed grid.
+// Grid-wide "last block" election for deterministic reductions.  Each
+// block stores its NV partials (sc1), drains, and takes a ticket; the block
+// that completes the grid reads every partial back (sc1) and sums them in
+// block order.  Tickets go through TICK_SUB sub-counters (block % TICK_SUB,
+// 256 B apart) whose last arrivals take a ticket on the top counter: one
+// address serialises ~10 ns per same-address atomic, so a flat counter
+// costs ~30 us for 3000 blocks.  tick: TICK_WORDS zeroed words, zero at rest.
+constexpr int TICK_SUB = 32;
+constexpr int TICK_STRIDE = 64;  // words
+constexpr int TICK_WORDS = (TICK_SUB + 1) * TICK_STRIDE;
 template <int NV>
-__device__ __forceinline__ bool last_block(const double (&v)[NV], double *part, unsigned *counter,
-                                           double (&tot)[NV]) {
+__device__ __forceinline__ bool last_block(const double (&v)[NV], double *part, unsigned *tick, double (&tot)[NV]) {
   __shared__ int s_last;
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int k = 0; k < NV; k++)
       __hip_atomic_store(&part[(size_t)blockIdx.x * NV + k], v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (t == gridDim.x - 1);
+    const unsigned g = blockIdx.x % TICK_SUB;
+    const unsigned members = (gridDim.x - g + TICK_SUB - 1) / TICK_SUB;
+    unsigned *sub = tick + (1 + g) * TICK_STRIDE;
+    int last = 0;
+    if (__hip_atomic_fetch_add(sub, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1) {
+      __hip_atomic_store(sub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned groups = gridDim.x < (unsigned)TICK_SUB ? gridDim.x : (unsigned)TICK_SUB;
+      last = __hip_atomic_fetch_add(tick, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == groups - 1;
+    }
+    s_last = last;
   }
   __syncthreads();
   if (!s_last) return false;
@@ -313,7 +329,7 @@ __device__ __forceinline__ bool last_block(const double (&v)[NV], double *part, 
   }
 #pragma unroll
   for (int k = 0; k < NV; k++) tot[k] = block_sum(x[k]);
-  if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_store(tick, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
 }
 
@@ -350,6 +366,7 @@ template <typename real> struct Fin {
   unsigned *cnt;   // zero at rest; arrival tickets of multi-part columns
   CgState *st;
   double *part;
+  unsigned *tick;  // last_block tickets (TICK_WORDS, zero at rest)
   int *run_host;
   int it;          // CG iteration (Hessian-vector mode)
 };
@@ -450,7 +467,7 @@ __device__ __forceinline__ void col_finalize(const Fin<real> &f, uint32_t col, v
 template <typename real, int MODE>
 __device__ __forceinline__ void fin_blocks(const Fin<real> &f, const double (&ds)[3]) {
   double bv[3] = {block_sum(ds[0]), block_sum(ds[1]), block_sum(ds[2])}, tot[3];
-  if (last_block<3>(bv, f.part, &f.st->counter, tot) && threadIdx.x == 0) {
+  if (last_block<3>(bv, f.part, f.tick, tot) && threadIdx.x == 0) {
     CgState *st = f.st;
     if (MODE == 0) {
       st->g2 = tot[0];
@@ -842,7 +859,7 @@ __global__ __launch_bounds__(BLOCK) void k_hs_cross_seg(uint64_t nseg, const Seg
 // MODE 0: gradient finalisation, MODE 1: Hessian-vector finalisation of CG
 // iteration f.it (col_finalize above), MODE 2: store the column sums into
 // f.acc (multi-GPU: the all-reduce and k_fin follow).
-template <typename real, int KP, int MODE>
+template <typename real, int KP, int MODE, int JE = JOB_ENT>
 __global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__restrict__ jobs,
                                                 const uint32_t *__restrict__ crow, const real *__restrict__ cval,
                                                 const real *__restrict__ h, uint64_t hbytes, real *__restrict__ wpart,
@@ -856,32 +873,35 @@ __global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__res
   const uint64_t wave = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
   const int sg = lane / G::LPR, li = lane % G::LPR;
   double dsum[3] = {0, 0, 0};
-  if (wave < nwave) {
-    const Job jb = jobs[wave * G::NSG + sg];
+  const uint64_t nwaves = ((uint64_t)gridDim.x * BLOCK) >> 6;
+  Job nxt = wave < nwave ? jobs[wave * G::NSG + sg] : Job{JOB_NONE, 1u, 0u, 0u, 0, 0};
+  for (uint64_t w = wave; w < nwave; w += nwaves) {
+    const Job jb = nxt;  // this round's job; the next round's is in flight below
+    if (w + nwaves < nwave) nxt = jobs[(w + nwaves) * G::NSG + sg];
     // finalisation operands first (padding jobs read column 0, unused)
     FinOps<real> ops;
     if (MODE != 2) ops = fin_load<real, KP, (MODE == 2 ? 0 : MODE)>(f, jb.col == JOB_NONE ? 0u : jb.col, upd, li);
-    constexpr int U = (JOB_ENT + G::LPR - 1) / G::LPR;
+    constexpr int U = (JE + G::LPR - 1) / G::LPR;
     uint32_t rr[U];
     real vv[U];
 #pragma unroll
     for (int t = 0; t < U; t++) {
       const int e = li + t * G::LPR;
-      const bool ok = e < JOB_ENT && jb.b + e < jb.e;
+      const bool ok = e < JE && jb.b + e < jb.e;
       rr[t] = ok ? crow[jb.b + e] : 0u;
       vv[t] = ok ? cval[jb.b + e] : (real)0;
     }
-    vec_t<real> hv[JOB_ENT];
-#pragma unroll
-    for (int e = 0; e < JOB_ENT; e++) {
-      const uint32_t r = __shfl(rr[e / G::LPR], sg * G::LPR + e % G::LPR, 64);
-      const real x = __shfl(vv[e / G::LPR], sg * G::LPR + e % G::LPR, 64);
+    vec_t<real> hv[JE];
+    sfor<JE>([&](auto E) {
+      constexpr int e = decltype(E)::value;
+      const uint32_t r = sg_bcast<G::LPR, e % G::LPR>(rr[e / G::LPR], li);
+      const real x = sg_bcast<G::LPR, e % G::LPR>(vv[e / G::LPR], li);
       const uint32_t off = jb.b + e < jb.e ? r * (uint32_t)(KP * sizeof(real)) + li * 16u : hb.oob;
       hv[e] = vsplat<real>(x) * bld<real>(hb, off);
-    }
+    });
     vec_t<real> s = hv[0];
 #pragma unroll
-    for (int e = 1; e < JOB_ENT; e++) s += hv[e];
+    for (int e = 1; e < JE; e++) s += hv[e];
     bool mine = jb.col != JOB_NONE;
     if (jb.flags & 1u) {  // wave job (wave-uniform)
       s = xsg_vsum<G::LPR, real>(s);

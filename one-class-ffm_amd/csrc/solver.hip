@@ -376,6 +376,7 @@ template <typename real> class Problem final : public ProblemBase {
     for (DevSide<real> *sd : {&U_, &V_})
       for (auto &F : sd->F) nslot = std::max(nslot, std::max(F->nslot, F->snslot));
     wpart_.alloc(nslot * kp_);
+    tick_.alloc(TICK_WORDS);
     C_ = fu_ * fv_;
     M_.alloc(std::max<uint32_t>(C_, 1) * kp_ * kp_);
     QTQ_.alloc((size_t)kp_ * kp_);
@@ -1188,6 +1189,7 @@ template <typename real> class Problem final : public ProblemBase {
     f.cnt = h.F->cnt.p;
     f.st = st_.p;
     f.part = part_.p;
+    f.tick = tick_.p;
     f.run_host = run_host_dev_;
     f.it = it;
     return f;
@@ -1216,7 +1218,7 @@ template <typename real> class Problem final : public ProblemBase {
       const double vecs = mode == 2 ? 1 : (mode == 0 ? 5 : (it > 1 ? 8 : 3));
       const double bytes = (double)ent * (4 + rs) + (double)ent * KP * rs + (double)njw * Gm::NSG * sizeof(Job) +
                            (double)h.D * KP * rs * vecs;
-      const unsigned grid = (unsigned)((njw + 3) / 4);
+      const unsigned grid = (unsigned)std::min<uint64_t>((njw + 3) / 4, 1024);  // grid-stride: fewer tickets
       const Fin<real> fin = make_fin(h, it);
       const Job *jobs = seg ? F.sjobs.p : F.jobs.p;
       const uint32_t *crow = seg ? F.scrow.p : F.crow.p;
@@ -1429,6 +1431,7 @@ template <typename real> class Problem final : public ProblemBase {
   std::vector<Block> blocks_;
   std::vector<DevBuf<real>> W_, H_, P_, Q_;
   DevBuf<real> acc_, G_, S_, Vd_, Rv_, Hv_, h_, M_, QTQ_, wpart_;
+  DevBuf<unsigned> tick_;
   DevBuf<double> sums_, vecs_, part_, at_d_, popular_;
   DevBuf<uint8_t> cold_;
   DevBuf<CgState> st_;

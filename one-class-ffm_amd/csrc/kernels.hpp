@@ -183,6 +183,12 @@ template <int N, typename F> __device__ __forceinline__ void sfor(F &&f) {
   sfor_impl(f, typename make_iseq<N>::type{});
 }
 
+// x M for a k-vector x spread over the subgroup (lane l holds components
+// l*VE ..) and a KP x KP row-major M (LDS or global): component e of x is
+// broadcast from its lane by DPP, M's row e read as one vector per lane.
+template <typename real, int KP>
+__device__ __forceinline__ vec_t<real> sg_vecmat(const vec_t<real> &x, const real *M, int li);
+
 // Raw-buffer view of a table for gathers.  A load at an out-of-range offset
 // returns zero without a memory access (the buffer range check), so the
 // unused slots of a fixed-width gather need neither a branch nor a wait:
@@ -204,6 +210,18 @@ template <> __device__ __forceinline__ float bld1<float>(const BufView &b, uint3
 }
 template <> __device__ __forceinline__ double bld1<double>(const BufView &b, uint32_t off) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(b.r, off, 0, 0));
+}
+
+template <typename real, int KP>
+__device__ __forceinline__ vec_t<real> sg_vecmat(const vec_t<real> &x, const real *M, int li) {
+  using G = Geo<real, KP>;
+  vec_t<real> t = vzero<real>();
+  sfor<KP>([&](auto E) {
+    constexpr int e = decltype(E)::value;
+    const real xe = sg_bcast<G::LPR, e / G::VE>(x[e % G::VE], li);
+    t += vsplat<real>(xe) * vld<real>(M + (size_t)e * KP + li * G::VE);
+  });
+  return t;
 }
 
 // A pass over up to PW positions [p0, p0+PW) of a positive segment, spread
@@ -659,11 +677,8 @@ __global__ __launch_bounds__(BLOCK) void k_gd_cross_seg(uint64_t nseg, const Seg
     }
     if (seg_first(sgm)) {
       vec_t<real> t = vzero<real>();
-      for (int c = 0; c < C; c++) {
-        const real *prow = Ptabs[c] + i * KP;
-#pragma unroll 4
-        for (int e = 0; e < KP; e++) t += vsplat<real>(prow[e]) * vld<real>(Mp + ((size_t)c * KP + e) * KP + li * G::VE);
-      }
+      for (int c = 0; c < C; c++)
+        t += sg_vecmat<real, KP>(vld<real>(Ptabs[c] + i * KP + li * G::VE), Mp + (size_t)c * KP * KP, li);
       const real z = ai - (real)r;
       pk += vsplat<real>((real)w) * (t + vsplat<real>(z) * oQ + bQ);
     }
@@ -773,8 +788,8 @@ __global__ __launch_bounds__(BLOCK) void k_hs_side_row(uint64_t R, const int64_t
 
 // Per segment of row i: h[s] = (1-w) sum_{j in seg} <phi_i, q_j> q_j
 // + [first] w phi_i QTQ, phi_i = X_i p  (hs_cross row body, ffm.cpp:715-738;
-// tau = X_i (V QTQ) = phi_i QTQ).  QTQ staged in LDS; phi of a first
-// segment staged per subgroup for the broadcast reads of the k x k product.
+// tau = X_i (V QTQ) = phi_i QTQ).  QTQ staged in LDS; phi_i's components
+// are broadcast by DPP for the k x k product (sg_vecmat).
 template <typename real, int KP, bool MLDS, bool FUSE>
 __global__ __launch_bounds__(BLOCK) void k_hs_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                         const int64_t *__restrict__ xptr,
@@ -794,7 +809,6 @@ __global__ __launch_bounds__(BLOCK) void k_hs_cross_seg(uint64_t nseg, const Seg
   const real alpha = upd ? (real)st->alpha : (real)0, beta = upd ? (real)st->beta : (real)0;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   real *Qs = reinterpret_cast<real *>(smem_raw);
-  real *phis = Qs + (MLDS ? KP * KP : 0);
   const real *Qp = QTQ;
   if (MLDS) {
     for (int t = threadIdx.x; t < KP * KP; t += BLOCK) Qs[t] = QTQ[t];
@@ -803,7 +817,6 @@ __global__ __launch_bounds__(BLOCK) void k_hs_cross_seg(uint64_t nseg, const Seg
   }
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
-  real *myphi = phis + (threadIdx.x / G::LPR) * KP;
   const real cpos = (real)(1 - w);
   double dsum[3] = {0, 0, 0};
   for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) {
@@ -833,13 +846,7 @@ __global__ __launch_bounds__(BLOCK) void k_hs_cross_seg(uint64_t nseg, const Seg
     }
     vec_t<real> out = vsplat<real>(cpos) * ka;
     if (seg_first(sgm)) {
-      vst<real>(myphi + li * G::VE, phi);
-      __builtin_amdgcn_wave_barrier();
-      vec_t<real> tau = vzero<real>();
-#pragma unroll 4
-      for (int e = 0; e < KP; e++) tau += vsplat<real>(myphi[e]) * vld<real>(Qp + (size_t)e * KP + li * G::VE);
-      __builtin_amdgcn_wave_barrier();
-      out += vsplat<real>((real)w) * tau;
+      out += vsplat<real>((real)w) * sg_vecmat<real, KP>(phi, Qp, li);
     }
     if (!FUSE) {
       vst<real>(h + s * KP + li * G::VE, out);

@@ -1271,7 +1271,7 @@ template <typename real> class Problem final : public ProblemBase {
         if (h.cross) {
           const size_t qsz = (size_t)KP * KP * sizeof(real);
           const bool lds = qsz <= 32 * 1024;
-          const size_t smem = (lds ? qsz : 0) + (size_t)(BLOCK / Gm::LPR) * KP * sizeof(real);
+          const size_t smem = lds ? qsz : 0;
           const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
                                (double)own.npos * 4 + (double)h.partner->R * KP * rs + (double)own.R * KP * rs;
           auto go = [&](auto fz, auto ml) {

@@ -988,8 +988,10 @@ __global__ __launch_bounds__(BLOCK) void k_apply(uint64_t nv, const real *__rest
 
 // ------------------------------------------------------- update rows ---
 // Per segment of row i (one segment per subgroup): XS_i = X_i S;
-// [first] P_i += XS_i; base_ij += <XS_i, q_j> for the segment's positives, in
-// both orientations (update_cross, ffm.cpp:439-465).
+// [first] P_i += XS_i; base_ij += <XS_i, q_j> for the segment's positives
+// (update_cross, ffm.cpp:439-465), in this side's orientation; k_gather_pos
+// then refreshes the other orientation (a gather instead of a scattered
+// read-modify-write per positive).
 template <typename real, int KP>
 __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                             const int64_t *__restrict__ xptr,
@@ -997,9 +999,8 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
                                                             const real *__restrict__ xval,
                                                             const real *__restrict__ S, real *__restrict__ P1,
                                                             const uint32_t *__restrict__ ycol,
-                                                            real *__restrict__ yt, real *__restrict__ yt_other,
-                                                            const uint32_t *__restrict__ perm,
-                                                            const real *__restrict__ Q1, uint64_t q1rows) {
+                                                            real *__restrict__ yt, const real *__restrict__ Q1,
+                                                            uint64_t q1rows) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP>;
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real));
@@ -1013,9 +1014,8 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
       xs += vsplat<real>(xval[p]) * vld<real>(S + (size_t)xidx[p] * KP + li * G::VE);
     if (seg_first(sgm)) vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
     for (int64_t p0 = sgm.b; p0 < sgm.e; p0 += PP::PW) {
-      uint32_t jj[PP::UT], pp[PP::UT];
+      uint32_t jj[PP::UT];
       PP::load_cols(ycol, p0, sgm.e, li, jj);
-      PP::load_cols(perm, p0, sgm.e, li, pp);
       real dd[PP::UT];
 #pragma unroll
       for (int t = 0; t < PP::UT; t++) dd[t] = 0;
@@ -1034,22 +1034,37 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
         }
       });
       // each lane owns its positions p0 + li + t*LPR: all loads, then all stores
-      // (distinct positives: the scattered targets never alias)
-      real yo[PP::UT], ym[PP::UT];
+      real ym[PP::UT];
 #pragma unroll
       for (int t = 0; t < PP::UT; t++) {
         const int64_t q = p0 + li + t * G::LPR;
         ym[t] = q < sgm.e ? yt[q] : (real)0;
-        yo[t] = q < sgm.e ? yt_other[pp[t]] : (real)0;
       }
 #pragma unroll
       for (int t = 0; t < PP::UT; t++) {
         const int64_t q = p0 + li + t * G::LPR;
-        if (q < sgm.e) {
-          yt[q] = ym[t] + dd[t];
-          yt_other[pp[t]] = yo[t] + dd[t];
-        }
+        if (q < sgm.e) yt[q] = ym[t] + dd[t];
       }
+    }
+  }
+}
+
+// dst[q] = src[idx[q]]: the other orientation of base from this one (idx =
+// the other side's perm).  Four positions per thread: one 16-B index load,
+// four gathers, one wide store.
+template <typename real>
+__global__ __launch_bounds__(BLOCK) void k_gather_pos(uint64_t n, const uint32_t *__restrict__ idx,
+                                                      const real *__restrict__ src, real *__restrict__ dst) {
+  for (uint64_t q = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) * 4; q < n; q += (uint64_t)gridDim.x * BLOCK * 4) {
+    if (q + 4 <= n) {
+      const uint4 ix = *reinterpret_cast<const uint4 *>(idx + q);
+      const real a = src[ix.x], b = src[ix.y], c = src[ix.z], d = src[ix.w];
+      dst[q] = a;
+      dst[q + 1] = b;
+      dst[q + 2] = c;
+      dst[q + 3] = d;
+    } else {
+      for (uint64_t r = q; r < n; r++) dst[r] = src[idx[r]];
     }
   }
 }

@@ -1175,6 +1175,15 @@ template <typename real> class Problem final : public ProblemBase {
   // subgroups per wave of this problem's row geometry (kernels.hpp: Geo)
   int nsg() const { return 64 / std::max<int>(1, (int)(kp_ * sizeof(real) / 16)); }
 
+  // other.yt (base in the other orientation) := own.yt through other.perm.
+  void refresh_other(DevSide<real> &own, DevSide<real> &other) {
+    if (!other.npos) return;
+    prof_launch("refresh_base", (double)other.npos * (4 + 2 * sizeof(real)), [&] {
+      launch(k_gather_pos<real>, grid_for((other.npos + 3) / 4, BLOCK, 4096), BLOCK, 0, (uint64_t)other.npos,
+             other.perm.p, own.yt.p, other.yt.p);
+    });
+  }
+
   Fin<real> make_fin(const HalfCtx &h, int it) {
     Fin<real> f;
     f.fw = h.fw;
@@ -1364,13 +1373,14 @@ template <typename real> class Problem final : public ProblemBase {
       if (h.cross) {
         DevSide<real> &other = *h.partner;
         const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
-                             (double)own.R * KP * rs * 2 + (double)own.npos * (4 + 4 + 4 * rs) +
+                             (double)own.R * KP * rs * 2 + (double)own.npos * (4 + 2 * rs) +
                              (double)other.R * KP * rs;
         prof_launch("update_cross_row", bytes, [&] {
           launch(k_update_cross_seg<real, KP>, grid_for(own.nseg, 4 * Gm::NSG), BLOCK, 0,
-              own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, own.ycol.p, own.yt.p, other.yt.p,
-              own.perm.p, h.Q1, (uint64_t)other.R);
+              own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, own.ycol.p, own.yt.p, h.Q1,
+              (uint64_t)other.R);
         });
+        refresh_other(own, other);
       } else {
         DevSide<real> &other = h.user ? V_ : U_;
         const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +

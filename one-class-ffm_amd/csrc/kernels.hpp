@@ -760,7 +760,7 @@ __global__ __launch_bounds__(BLOCK) void k_hs_side_row(uint64_t R, const int64_t
                                                        const real *__restrict__ Q1, double w, double n1,
                                                        real *__restrict__ h, const int *__restrict__ run,
                                                        const real *__restrict__ Rv, const real *__restrict__ Hv,
-                                                       const CgState *st, int it, Fin<real> f) {
+                                                       const CgState *st, int it, bool one, Fin<real> f) {
   using G = Geo<real, KP>;
   if (run && !*run) return;
   const bool upd = st && it > 1;
@@ -770,8 +770,12 @@ __global__ __launch_bounds__(BLOCK) void k_hs_side_row(uint64_t R, const int64_t
   double dsum[3] = {0, 0, 0};
   for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
     vec_t<real> phi = vzero<real>();
-    for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
-      phi += vsplat<real>(xval[p]) * cg_dir_at<real, KP>(V, Rv, Hv, alpha, beta, upd, (size_t)xidx[p] * KP + li * G::VE);
+    if (one) {  // one node per row: xptr[i] == i
+      phi = vsplat<real>(xval[i]) * cg_dir_at<real, KP>(V, Rv, Hv, alpha, beta, upd, (size_t)xidx[i] * KP + li * G::VE);
+    } else {
+      for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
+        phi += vsplat<real>(xval[p]) * cg_dir_at<real, KP>(V, Rv, Hv, alpha, beta, upd, (size_t)xidx[p] * KP + li * G::VE);
+    }
     const vec_t<real> q = vld<real>(Q1 + i * KP + li * G::VE);
     const real z = sg_sum<G::LPR>(hsum<real>(phi * q));
     const real d = (real)((1 - w) * (double)(yptr[i + 1] - yptr[i]) + w * n1);
@@ -800,7 +804,8 @@ __global__ __launch_bounds__(BLOCK) void k_hs_cross_seg(uint64_t nseg, const Seg
                                                         const real *__restrict__ QTQ, double w, real *__restrict__ h,
                                                         const int *__restrict__ run, const real *__restrict__ Rv,
                                                         const real *__restrict__ Hv, const CgState *st, int it,
-                                                        Fin<real> f) {
+                                                        const uint32_t *__restrict__ segd,
+                                                        const real *__restrict__ segx, Fin<real> f) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP, 32>;  // 32 gathers in flight per subgroup: latency-bound
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real));
@@ -823,8 +828,12 @@ __global__ __launch_bounds__(BLOCK) void k_hs_cross_seg(uint64_t nseg, const Seg
     const Seg sgm = segs[s];
     const uint64_t i = sgm.row;
     vec_t<real> phi = vzero<real>();
-    for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
-      phi += vsplat<real>(xval[p]) * cg_dir_at<real, KP>(V, Rv, Hv, alpha, beta, upd, (size_t)xidx[p] * KP + li * G::VE);
+    if (segd) {  // one node per row: the segment carries it (no row indirection)
+      phi = vsplat<real>(segx[s]) * cg_dir_at<real, KP>(V, Rv, Hv, alpha, beta, upd, (size_t)segd[s] * KP + li * G::VE);
+    } else {
+      for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
+        phi += vsplat<real>(xval[p]) * cg_dir_at<real, KP>(V, Rv, Hv, alpha, beta, upd, (size_t)xidx[p] * KP + li * G::VE);
+    }
     vec_t<real> ka = vzero<real>();
     for (int64_t p0 = sgm.b; p0 < sgm.e; p0 += PP::PW) {
       uint32_t jj[PP::UT];
@@ -1000,7 +1009,8 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
                                                             const real *__restrict__ S, real *__restrict__ P1,
                                                             const uint32_t *__restrict__ ycol,
                                                             real *__restrict__ yt, const real *__restrict__ Q1,
-                                                            uint64_t q1rows) {
+                                                            uint64_t q1rows, const uint32_t *__restrict__ segd,
+                                                            const real *__restrict__ segx) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP>;
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real));
@@ -1010,8 +1020,12 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
     const Seg sgm = segs[s];
     const uint64_t i = sgm.row;
     vec_t<real> xs = vzero<real>();
-    for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
-      xs += vsplat<real>(xval[p]) * vld<real>(S + (size_t)xidx[p] * KP + li * G::VE);
+    if (segd) {
+      xs = vsplat<real>(segx[s]) * vld<real>(S + (size_t)segd[s] * KP + li * G::VE);
+    } else {
+      for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
+        xs += vsplat<real>(xval[p]) * vld<real>(S + (size_t)xidx[p] * KP + li * G::VE);
+    }
     if (seg_first(sgm)) vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
     for (int64_t p0 = sgm.b; p0 < sgm.e; p0 += PP::PW) {
       uint32_t jj[PP::UT];
@@ -1078,14 +1092,18 @@ __global__ __launch_bounds__(BLOCK) void k_update_side_row(uint64_t R, const int
                                                            const uint32_t *__restrict__ xidx,
                                                            const real *__restrict__ xval, const real *__restrict__ S,
                                                            real *__restrict__ P1, const real *__restrict__ Q1,
-                                                           real *__restrict__ a1) {
+                                                           real *__restrict__ a1, bool one) {
   using G = Geo<real, KP>;
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
   for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
     vec_t<real> xs = vzero<real>();
-    for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
-      xs += vsplat<real>(xval[p]) * vld<real>(S + (size_t)xidx[p] * KP + li * G::VE);
+    if (one) {
+      xs = vsplat<real>(xval[i]) * vld<real>(S + (size_t)xidx[i] * KP + li * G::VE);
+    } else {
+      for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
+        xs += vsplat<real>(xval[p]) * vld<real>(S + (size_t)xidx[p] * KP + li * G::VE);
+    }
     vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
     const real gap = sg_sum<G::LPR>(hsum<real>(xs * vld<real>(Q1 + i * KP + li * G::VE)));
     if (li == 0) a1[i] += gap;

@@ -149,6 +149,9 @@ template <typename real> struct DevField {
   uint64_t snjw = 0, snslot = 0;
   DevBuf<unsigned> cnt;  // per-column arrival tickets (zero at rest)
   bool idlike = false;   // one node per row and each feature in exactly one row (CSC = identity)
+  bool one = false;      // exactly one node per row (xptr[i] == i)
+  DevBuf<uint32_t> segd;  // one: the node of each positive segment's row (no row indirection)
+  DevBuf<real> segx;
   // host copies kept until the segment CSC is built
   std::vector<int64_t> h_xptr;
   std::vector<uint32_t> h_xidx;
@@ -194,6 +197,11 @@ template <typename real> static void build_seg_csc(DevSide<real> &s, const std::
       }
     std::vector<uint32_t> crow;
     std::vector<double> cval;
+    if (F.one) {  // xidx/xval now hold one node per segment
+      F.segd.upload(xidx);
+      std::vector<real> sx(xval.begin(), xval.end());
+      F.segx.upload(sx);
+    }
     std::vector<Job> jobs;
     build_csc(sidx, F.D, xptr.data(), xidx.data(), xval.data(), nsg, crow, cval, jobs, F.snslot);
     F.scrow.upload(crow);
@@ -729,6 +737,8 @@ template <typename real> class Problem final : public ProblemBase {
         xval.assign(d.xval[fi].begin() + base, d.xval[fi].begin() + d.xptr[fi][r1]);
       }
       F->nnz = xidx.size();
+      F->one = R > 0 && F->nnz == R;
+      for (uint64_t i = 0; i < R && F->one; i++) F->one = xptr[i + 1] - xptr[i] == 1;
       if (F->nnz == R && F->D == R && R > 0) {
         std::vector<uint8_t> seen(F->D, 0);
         bool ok = true;
@@ -1287,7 +1297,7 @@ template <typename real> class Problem final : public ProblemBase {
             constexpr bool FZ = decltype(fz)::value, ML = decltype(ml)::value;
             launch(k_hs_cross_seg<real, KP, ML, FZ>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, smem, own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p,
                                                          own.ycol.p, h.Q1, (uint64_t)h.partner->R, QTQ_.p, w_, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
-                                                         fin);
+                                                         F.segd.p, F.segx.p, fin);
           };
           prof_launch(fz_ ? "hs_cross_fused" : "hs_cross_row", bytes, [&] {
             if (fz_) {
@@ -1307,7 +1317,7 @@ template <typename real> class Problem final : public ProblemBase {
             constexpr bool FZ = decltype(fz)::value;
             launch(k_hs_side_row<real, KP, FZ>, grid_for(own.R, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, 0,
                 own.R, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.yptr.p, h.Q1, w_, n1, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
-                fin);
+                F.one, fin);
           };
           prof_launch(fz_ ? "hs_side_fused" : "hs_side_row", bytes, [&] {
             if (fz_) go(std::true_type());
@@ -1378,7 +1388,7 @@ template <typename real> class Problem final : public ProblemBase {
         prof_launch("update_cross_row", bytes, [&] {
           launch(k_update_cross_seg<real, KP>, grid_for(own.nseg, 4 * Gm::NSG), BLOCK, 0,
               own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, own.ycol.p, own.yt.p, h.Q1,
-              (uint64_t)other.R);
+              (uint64_t)other.R, F.segd.p, F.segx.p);
         });
         refresh_other(own, other);
       } else {
@@ -1387,7 +1397,7 @@ template <typename real> class Problem final : public ProblemBase {
                              (double)own.R * KP * rs * 3 + (double)own.R * rs * 2 + (double)own.npos * (4 + 4 * rs);
         prof_launch("update_side_row", bytes, [&] {
           launch(k_update_side_row<real, KP>, grid_for(own.R, 4 * Gm::NSG), BLOCK, 0,
-              own.R, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, h.Q1, own.bias.p);
+              own.R, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, h.Q1, own.bias.p, F.one);
         });
       }
     });

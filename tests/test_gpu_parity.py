@@ -174,6 +174,28 @@ def test_kkbox_small_fp64(kk_small):
     np.testing.assert_allclose(vg["prec"], vo["prec"], atol=1e-12)
 
 
+@pytest.mark.parametrize("precision", [ocffm.FP64, ocffm.FP32])
+def test_heavy_columns(precision):
+    """Low-cardinality fields: columns with hundreds of rows go through the
+    feature pass as several wave-chunks summed by the last to arrive
+    (kernels.hpp: Job), in both the row and the segment CSC."""
+    ds = synth.general(seed=13, m=1500, n=300, fu=2, fv=2, k=8, d_user=[1500, 3], d_item=[300, 2], nnz_user=1,
+                       mean_pos=12.0, vals="real")
+    o, g = pair(ds, precision=precision, with_test=False)
+    for _ in range(2):
+        o.one_epoch()
+        g.one_epoch()
+    if precision == ocffm.FP64:
+        assert_state(o, g, 1e-9)
+        np.testing.assert_array_equal(g.cg_log(), o.cg_log())
+    else:
+        f_ref = o.func()
+        o2 = O.Oracle(ds, with_test=False)
+        ocffm.srand(1)
+        o2.init()
+        assert abs(gpu_objective(o2, g) - f_ref) <= 1e-3 * abs(f_ref)
+
+
 @pytest.mark.parametrize("env", [{"OCFFM_FUSE": "1"}, {"OCFFM_SEG_LEN": "3"}, {"OCFFM_LOOKAHEAD": "3"},
                                  {"OCFFM_FUSE": "1", "OCFFM_SEG_LEN": "2"}])
 def test_execution_variants_fp64(kk_small, monkeypatch, env):

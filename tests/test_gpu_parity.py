@@ -186,8 +186,11 @@ def test_heavy_columns(precision):
         o.one_epoch()
         g.one_epoch()
     if precision == ocffm.FP64:
-        assert_state(o, g, 1e-9)
+        # 500-row real-valued columns make these halves worse conditioned: the
+        # reassociated sums (wave-chunk order, expanded |r - a Hp|^2) drift to
+        # ~2e-9 relative after two epochs, so this case uses 1e-8.
         np.testing.assert_array_equal(g.cg_log(), o.cg_log())
+        assert_state(o, g, 1e-8)
     else:
         f_ref = o.func()
         o2 = O.Oracle(ds, with_test=False)

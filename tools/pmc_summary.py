@@ -15,20 +15,20 @@ import re
 import sys
 from collections import defaultdict
 
-FAMILY = [
-    ("k_hs_cross_seg", "hs_cross_row"), ("k_hs_side_row", "hs_side_row"), ("k_feat<float, 32, 1>", "feat_hv"),
-    ("k_feat<double, 32, 1>", "feat_hv"), ("k_feat<float, 32, 0>", "feat_grad"), ("k_feat<double, 32, 0>", "feat_grad"),
-("k_gd_cross_seg", "gd_cross_row"), ("k_gd_side_seg", "gd_side_row"),
-    ("k_update_cross_seg", "update_cross_row"), ("k_update_side_row", "update_side_row"),
-    ("k_gram_part", "aggregates"), ("k_reduce_parts", "aggr_reduce"), ("k_apply", "apply_step"),
-    ("k_rowdot_multi", "rowdot_multi"), ("k_csc", "csc_scatter"), ("k_fin<float, 32, 1>", "hv_fin"),
-    ("k_fin<double, 32, 1>", "hv_fin"), ("k_fin<float, 32, 0>", "grad_fin"), ("k_fin<double, 32, 0>", "grad_fin"),
+FAMILY = [  # (regex on the demangled kernel name, family as named by the library's profiler)
+    (r"k_hs_cross_seg", "hs_cross_row"), (r"k_hs_side_row", "hs_side_row"),
+    (r"k_feat<\w+, \d+, 1\b", "feat_hv"), (r"k_feat<\w+, \d+, 0\b", "feat_grad"),
+    (r"k_feat<\w+, \d+, 2\b", "csc_scatter"), (r"k_fin<\w+, \d+, 0\b", "grad_fin"),
+    (r"k_fin<\w+, \d+, 1\b", "hv_fin"), (r"k_gd_cross_seg", "gd_cross_row"), (r"k_gd_side_seg", "gd_side_row"),
+    (r"k_update_cross_seg", "update_cross_row"), (r"k_update_side_row", "update_side_row"),
+    (r"k_gather_pos", "refresh_base"), (r"k_gram_part", "aggregates"), (r"k_reduce_parts", "aggr_reduce"),
+    (r"k_apply", "apply_step"), (r"k_rowdot_multi", "rowdot_multi"),
 ]
 
 
 def family(name):
     for key, fam in FAMILY:
-        if key in name:
+        if re.search(key, name):
             return fam
     return re.sub(r"\(.*", "", name)
 

@@ -105,7 +105,9 @@ int ocffm_problem_create(const ocffm_data *U, const ocffm_data *Ut, const ocffm_
  * nranks contiguous shards and this rank keeps shard `rank`.  Gradient and
  * Hessian-vector partial sums are all-reduced with RCCL.
  * comm_id: OCFFM_COMM_ID_BYTES bytes from ocffm_comm_id() on rank 0,
- * broadcast by the caller.  Test rows (Ut) are sharded the same way. */
+ * broadcast by the caller (with nranks == 1 the RCCL path still runs: a
+ * one-rank communicator, used by the tests).  Test rows (Ut) are sharded
+ * the same way. */
 #define OCFFM_COMM_ID_BYTES 128
 int ocffm_comm_id(void *out);
 int ocffm_problem_create_dist(const ocffm_data *U, const ocffm_data *Ut, const ocffm_data *V,

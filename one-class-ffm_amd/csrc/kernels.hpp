@@ -368,8 +368,14 @@ template <typename real, int KP>
 __device__ __forceinline__ vec_t<real> cg_dir_at(const real *__restrict__ P, const real *__restrict__ Rv,
                                                  const real *__restrict__ Hv, real alpha, real beta, bool upd,
                                                  size_t off) {
-  if (!upd) return vld<real>(P + off);
-  return (vld<real>(Rv + off) - vsplat<real>(alpha) * vld<real>(Hv + off)) + vsplat<real>(beta) * vld<real>(P + off);
+  // branch-free: the three loads go out together (a select, not a branch,
+  // picks the formula; without upd the R/Hp rows are read but unused)
+  const vec_t<real> p = vld<real>(P + off), r = vld<real>(Rv + off), hp = vld<real>(Hv + off);
+  const vec_t<real> u = (r - vsplat<real>(alpha) * hp) + vsplat<real>(beta) * p;
+  vec_t<real> o;
+#pragma unroll
+  for (int e = 0; e < VT<real>::N; e++) o[e] = upd ? u[e] : p[e];
+  return o;
 }
 
 // ------------------------------------------------ column finalisation ---
@@ -807,7 +813,7 @@ __global__ __launch_bounds__(BLOCK) void k_hs_cross_seg(uint64_t nseg, const Seg
                                                         const uint32_t *__restrict__ segd,
                                                         const real *__restrict__ segx, Fin<real> f) {
   using G = Geo<real, KP>;
-  using PP = PosPass<real, KP, 32>;  // 32 gathers in flight per subgroup: latency-bound
+  using PP = PosPass<real, KP, 32>;  // one round of gathers per <= 32-positive segment
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real));
   if (run && !*run) return;
   const bool upd = st && it > 1;
@@ -824,20 +830,44 @@ __global__ __launch_bounds__(BLOCK) void k_hs_cross_seg(uint64_t nseg, const Seg
   const int sg = lane / G::LPR, li = lane % G::LPR;
   const real cpos = (real)(1 - w);
   double dsum[3] = {0, 0, 0};
-  for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) {
-    const Seg sgm = segs[s];
+  // Grid-stride over segments with the next segment's descriptor (and its
+  // node) in flight while the current one is gathered.
+  const uint64_t stride = nwaves * G::NSG;
+  uint64_t s = wave * G::NSG + sg;
+  Seg nxt{0u, 0u, 0, 0};
+  uint32_t nd = 0;
+  real nx = 0;
+  if (s < nseg) {
+    nxt = segs[s];
+    if (segd) {
+      nd = segd[s];
+      nx = segx[s];
+    }
+  }
+  for (; s < nseg; s += stride) {
+    const Seg sgm = nxt;
+    const uint32_t d1 = nd;
+    const real x1 = nx;
+    if (s + stride < nseg) {
+      nxt = segs[s + stride];
+      if (segd) {
+        nd = segd[s + stride];
+        nx = segx[s + stride];
+      }
+    }
     const uint64_t i = sgm.row;
+    uint32_t jj[PP::UT];  // the first pass's columns go out with the phi gather
+    PP::load_cols(ycol, sgm.b, sgm.e, li, jj);
     vec_t<real> phi = vzero<real>();
     if (segd) {  // one node per row: the segment carries it (no row indirection)
-      phi = vsplat<real>(segx[s]) * cg_dir_at<real, KP>(V, Rv, Hv, alpha, beta, upd, (size_t)segd[s] * KP + li * G::VE);
+      phi = vsplat<real>(x1) * cg_dir_at<real, KP>(V, Rv, Hv, alpha, beta, upd, (size_t)d1 * KP + li * G::VE);
     } else {
       for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
         phi += vsplat<real>(xval[p]) * cg_dir_at<real, KP>(V, Rv, Hv, alpha, beta, upd, (size_t)xidx[p] * KP + li * G::VE);
     }
     vec_t<real> ka = vzero<real>();
     for (int64_t p0 = sgm.b; p0 < sgm.e; p0 += PP::PW) {
-      uint32_t jj[PP::UT];
-      PP::load_cols(ycol, p0, sgm.e, li, jj);
+      if (p0 != sgm.b) PP::load_cols(ycol, p0, sgm.e, li, jj);
       sfor<PP::PW / PP::GB>([&](auto BT) {
         constexpr int bt = decltype(BT)::value * PP::GB;
         if (p0 + bt >= sgm.e) return;

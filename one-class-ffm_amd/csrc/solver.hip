@@ -317,7 +317,7 @@ struct Comm {
   ncclComm_t nccl = nullptr;
   ocffm_allreduce_fn host_fn = nullptr;
   void *host_user = nullptr;
-  bool active() const { return nranks > 1 || host_fn != nullptr; }
+  bool active() const { return nranks > 1 || host_fn != nullptr || nccl != nullptr; }
 };
 
 template <typename real> class Problem final : public ProblemBase {
@@ -342,6 +342,7 @@ template <typename real> class Problem final : public ProblemBase {
     n_ = V.m;
     if (const char *e = std::getenv("OCFFM_SEG_LEN")) seg_len_ = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
     if (const char *e = std::getenv("OCFFM_LOOKAHEAD")) lookahead_ = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("OCFFM_HS_BLOCKS")) hs_blocks_ = (unsigned)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("OCFFM_FUSE")) no_fuse_ = std::atoi(e) == 0;  // id-field row fusion: opt-in
     // shard users contiguously
     u0_ = U.m * (uint64_t)comm_.rank / (uint64_t)comm_.nranks;
@@ -1295,7 +1296,7 @@ template <typename real> class Problem final : public ProblemBase {
                                (double)own.npos * 4 + (double)h.partner->R * KP * rs + (double)own.R * KP * rs;
           auto go = [&](auto fz, auto ml) {
             constexpr bool FZ = decltype(fz)::value, ML = decltype(ml)::value;
-            launch(k_hs_cross_seg<real, KP, ML, FZ>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, smem, own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p,
+            launch(k_hs_cross_seg<real, KP, ML, FZ>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : hs_blocks_), BLOCK, smem, own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p,
                                                          own.ycol.p, h.Q1, (uint64_t)h.partner->R, QTQ_.p, w_, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
                                                          F.segd.p, F.segx.p, fin);
           };
@@ -1445,6 +1446,7 @@ template <typename real> class Problem final : public ProblemBase {
   uint64_t seg_len_ = 32;
   int lookahead_ = 1;
   bool no_fuse_ = true;
+  unsigned hs_blocks_ = 4096;  // grid cap of the cross Hessian-vector row pass
   hipEvent_t arm_a_ = nullptr, arm_b_ = nullptr;
   bool arm_first_ = false;
   DevSide<real> U_, V_, T_;
@@ -1630,7 +1632,7 @@ int ocffm_problem_create_dist(const ocffm_data *U, const ocffm_data *Ut, const o
     if (nranks < 1 || rank < 0 || rank >= nranks) throw Error(OCFFM_E_ARG, "bad rank/nranks");
     c.rank = rank;
     c.nranks = nranks;
-    if (nranks > 1) {
+    if (comm_id) {  // RCCL even for one rank: the distributed path, all-reduces included
       HIPCHK(hipSetDevice(p->device));
       ncclUniqueId id;
       std::memcpy(&id, comm_id, sizeof(id));

@@ -241,7 +241,7 @@ class ImpProblem:
             self._cb = ALLREDUCE_FN(cb)
             _check(lib().ocffm_problem_create_dist_host(U.h, uva, V.h, C.byref(param._p), rank, nranks, self._cb,
                                                         None, C.byref(h)))
-        elif nranks > 1:
+        elif nranks > 1 or comm is not None:
             idb = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(comm)
             _check(lib().ocffm_problem_create_dist(U.h, uva, V.h, C.byref(param._p), rank, nranks, idb,
                                                    C.byref(h)))

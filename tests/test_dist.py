@@ -203,3 +203,25 @@ def test_two_ranks_match_one_rank_on_gpu():
         assert abs(float(r0["loss"]) - met["loss"]) <= 1e-9 * met["loss"]
         np.testing.assert_allclose(r0["ndcg"], met["ndcg"], atol=1e-12)
         np.testing.assert_allclose(r0["prec"], met["prec"], atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_rccl_one_rank_matches_single():
+    """The RCCL code path (scatter pass, ncclAllReduce, k_fin) on a one-rank
+    communicator must reproduce the single-GPU fused path (fp64, 1e-9)."""
+    import ocffm
+    ds = synth.tiny(seed=8)
+    a = ocffm.problem_from_dataset(ds, precision=ocffm.FP64)
+    b = ocffm.problem_from_dataset(ds, precision=ocffm.FP64, rank=0, nranks=1, comm=ocffm.comm_id())
+    for g in (a, b):
+        ocffm.srand(1)
+        g.init()
+        for _ in range(2):
+            g.one_epoch()
+    np.testing.assert_array_equal(a.cg_log(), b.cg_log())
+    for bl in range(6):
+        for what in "WH":
+            ref = a.get(what, bl)
+            assert np.abs(b.get(what, bl) - ref).max() <= 1e-9 * np.abs(ref).max(), (what, bl)
+    ma, mb = a.validate(), b.validate()
+    assert abs(ma["loss"] - mb["loss"]) <= 1e-9 * ma["loss"]

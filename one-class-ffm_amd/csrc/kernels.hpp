@@ -393,6 +393,9 @@ template <typename real> struct Fin {
   unsigned *tick;  // last_block tickets (TICK_WORDS, zero at rest)
   int *run_host;
   int it;          // CG iteration (Hessian-vector mode)
+  double *dots;    // non-null: the grid's dot products are this rank's partials;
+                   // the last block stores them here for a cross-rank sum and
+                   // k_cg_step publishes the CG scalars (owned fields)
 };
 
 // A column receiving `nparts` partial sums: each part adds into acc and takes
@@ -489,35 +492,54 @@ __device__ __forceinline__ void col_finalize(const Fin<real> &f, uint32_t col, v
 // CG verdict; MODE 1 computes alpha = r2/<p,Hp>, the new r2 (expanded),
 // beta and the verdict for iteration it+1 (ffm.cpp:780, 803-809).
 template <typename real, int MODE>
+__device__ __forceinline__ void cg_publish(const Fin<real> &f, const double (&tot)[3]) {
+  CgState *st = f.st;
+  if (MODE == 0) {
+    st->g2 = tot[0];
+    st->r2 = tot[0];
+    st->nr_cg = 0;
+    for (int i = 0; i <= MAXCG + 1; i++) {
+      st->run[i] = 0;
+      if (f.run_host) __hip_atomic_store(f.run_host + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    const int go = (tot[0] * CG_EPS < tot[0]) ? 1 : 0;
+    st->run[1] = go;
+    if (f.run_host) __hip_atomic_store(f.run_host + 1, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+    const double r2 = st->r2;
+    const double alpha = r2 / tot[0];
+    const double r2n = r2 - 2 * alpha * tot[1] + alpha * alpha * tot[2];
+    st->vhv = tot[0];
+    st->alpha = alpha;
+    st->beta = r2n / r2;
+    st->r2 = r2n;
+    st->nr_cg = f.it;
+    const int go = (f.it < MAXCG && st->g2 * CG_EPS < r2n) ? 1 : 0;
+    st->run[f.it + 1] = go;
+    if (f.run_host) __hip_atomic_store(f.run_host + f.it + 1, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+template <typename real, int MODE>
 __device__ __forceinline__ void fin_blocks(const Fin<real> &f, const double (&ds)[3]) {
   double bv[3] = {block_sum(ds[0]), block_sum(ds[1]), block_sum(ds[2])}, tot[3];
   if (last_block<3>(bv, f.part, f.tick, tot) && threadIdx.x == 0) {
-    CgState *st = f.st;
-    if (MODE == 0) {
-      st->g2 = tot[0];
-      st->r2 = tot[0];
-      st->nr_cg = 0;
-      for (int i = 0; i <= MAXCG + 1; i++) {
-        st->run[i] = 0;
-        if (f.run_host) __hip_atomic_store(f.run_host + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-      const int go = (tot[0] * CG_EPS < tot[0]) ? 1 : 0;
-      st->run[1] = go;
-      if (f.run_host) __hip_atomic_store(f.run_host + 1, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (f.dots) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) f.dots[k] = tot[k];
     } else {
-      const double r2 = st->r2;
-      const double alpha = r2 / tot[0];
-      const double r2n = r2 - 2 * alpha * tot[1] + alpha * alpha * tot[2];
-      st->vhv = tot[0];
-      st->alpha = alpha;
-      st->beta = r2n / r2;
-      st->r2 = r2n;
-      st->nr_cg = f.it;
-      const int go = (f.it < MAXCG && st->g2 * CG_EPS < r2n) ? 1 : 0;
-      st->run[f.it + 1] = go;
-      if (f.run_host) __hip_atomic_store(f.run_host + f.it + 1, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      cg_publish<real, MODE>(f, tot);
     }
   }
+}
+
+// CG scalars of an owned-field feature pass once its partial dot products
+// have been summed over the ranks: one thread.
+template <typename real, int MODE>
+__global__ void k_cg_step(Fin<real> f) {
+  if (MODE == 1 && !f.st->run[f.it]) return;
+  const double tot[3] = {f.dots[0], f.dots[1], f.dots[2]};
+  cg_publish<real, MODE>(f, tot);
 }
 
 // ------------------------------------------------------------------ UTX ---
@@ -1014,14 +1036,28 @@ __global__ __launch_bounds__(BLOCK) void k_fin(uint64_t nv, Fin<real> f) {
 
 // The step of the half: S += alpha_last p_last (the update of the last CG
 // iteration, pending under the lazy scheme above), W += S  (ffm.cpp:806, 410, 441).
+// own (owned fields on several ranks): only this rank's feature rows; the
+// others hold another rank's stale scratch and are left alone.
 template <typename real>
 __global__ __launch_bounds__(BLOCK) void k_apply(uint64_t nv, const real *__restrict__ P, real *__restrict__ S,
-                                                 real *__restrict__ W, const CgState *st) {
+                                                 real *__restrict__ W, const CgState *st,
+                                                 const uint8_t *__restrict__ own, uint32_t lpr) {
   const real alpha = st->nr_cg >= 1 ? (real)st->alpha : (real)0;
   VEC_LOOP {
+    if (own && !own[v / lpr]) continue;
     const vec_t<real> s = vld<real>(S + v * VT<real>::N) + vsplat<real>(alpha) * vld<real>(P + v * VT<real>::N);
     vst<real>(S + v * VT<real>::N, s);
     vst<real>(W + v * VT<real>::N, vld<real>(W + v * VT<real>::N) + s);
+  }
+}
+
+// Zero the feature rows this rank does not own (owned fields before the
+// all-reduce that makes a table whole again on every rank).
+template <typename real>
+__global__ __launch_bounds__(BLOCK) void k_mask_rows(uint64_t nv, real *__restrict__ T, const uint8_t *__restrict__ own,
+                                                     uint32_t lpr) {
+  VEC_LOOP {
+    if (!own[v / lpr]) vst<real>(T + v * VT<real>::N, vzero<real>());
   }
 }
 

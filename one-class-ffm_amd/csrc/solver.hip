@@ -150,6 +150,13 @@ template <typename real> struct DevField {
   DevBuf<unsigned> cnt;  // per-column arrival tickets (zero at rest)
   bool idlike = false;   // one node per row and each feature in exactly one row (CSC = identity)
   bool one = false;      // exactly one node per row (xptr[i] == i)
+  // Owned field (several ranks): every feature is touched by the
+  // rows of at most one rank.  Its CG vectors are then not all-reduced: each
+  // rank finalises only the columns it owns (untouched ones go to rank 0) and
+  // only the dot products are summed over the ranks.
+  bool excl = false;
+  std::vector<uint8_t> h_own;
+  DevBuf<uint8_t> own;
   DevBuf<uint32_t> segd;  // one: the node of each positive segment's row (no row indirection)
   DevBuf<real> segx;
   // host copies kept until the segment CSC is built
@@ -203,7 +210,8 @@ template <typename real> static void build_seg_csc(DevSide<real> &s, const std::
       F.segx.upload(sx);
     }
     std::vector<Job> jobs;
-    build_csc(sidx, F.D, xptr.data(), xidx.data(), xval.data(), nsg, crow, cval, jobs, F.snslot);
+    build_csc(sidx, F.D, xptr.data(), xidx.data(), xval.data(), nsg, crow, cval, jobs, F.snslot,
+              F.excl ? F.h_own.data() : nullptr);
     F.scrow.upload(crow);
     std::vector<real> cv(cval.begin(), cval.end());
     F.scval.upload(cv);
@@ -250,10 +258,11 @@ struct Block {
 // Feature-major (CSC) view of one field's CSR and its feature-pass jobs
 // (kernels.hpp: Job): light columns first, packed NSG to a wave, then the
 // wave-chunks of the heavy columns.  Empty columns get a job too (their
-// finalisation is lam W alone).
+// finalisation is lam W alone).  own (owned fields): columns of other ranks
+// get no job.
 static void build_csc(uint64_t R, uint64_t D, const int64_t *xptr, const uint32_t *xidx, const double *xval, int nsg,
                       std::vector<uint32_t> &crow, std::vector<double> &cval, std::vector<Job> &jobs,
-                      uint64_t &nslot) {
+                      uint64_t &nslot, const uint8_t *own) {
   const uint64_t nnz = (uint64_t)xptr[R] - (uint64_t)xptr[0];
   std::vector<uint64_t> cptr(D + 1, 0);
   for (int64_t p = xptr[0]; p < xptr[R]; p++) cptr[xidx[p] + 1]++;
@@ -269,14 +278,14 @@ static void build_csc(uint64_t R, uint64_t D, const int64_t *xptr, const uint32_
     }
   jobs.clear();
   for (uint64_t d = 0; d < D; d++)
-    if (cptr[d + 1] - cptr[d] <= (uint64_t)JOB_ENT)
+    if (cptr[d + 1] - cptr[d] <= (uint64_t)JOB_ENT && (!own || own[d]))
       jobs.push_back(Job{(uint32_t)d, 1u, 0u, 0u, (int64_t)cptr[d], (int64_t)cptr[d + 1]});
   while (jobs.size() % nsg) jobs.push_back(Job{JOB_NONE, 1u, 0u, 0u, 0, 0});
   const uint64_t wc = (uint64_t)nsg * JOB_ENT;
   nslot = 0;
   for (uint64_t d = 0; d < D; d++) {
     const uint64_t b = cptr[d], e = cptr[d + 1];
-    if (e - b <= (uint64_t)JOB_ENT) continue;
+    if (e - b <= (uint64_t)JOB_ENT || (own && !own[d])) continue;
     const uint32_t np = (uint32_t)((e - b + wc - 1) / wc);
     for (uint32_t q = 0; q < np; q++)
       for (int g = 0; g < nsg; g++) {
@@ -344,6 +353,7 @@ template <typename real> class Problem final : public ProblemBase {
     if (const char *e = std::getenv("OCFFM_LOOKAHEAD")) lookahead_ = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("OCFFM_HS_BLOCKS")) hs_blocks_ = (unsigned)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("OCFFM_FUSE")) no_fuse_ = std::atoi(e) == 0;  // id-field row fusion: opt-in
+    if (const char *e = std::getenv("OCFFM_NO_OWNED")) no_owned_ = std::atoi(e) != 0;  // all-reduce every field
     // shard users contiguously
     u0_ = U.m * (uint64_t)comm_.rank / (uint64_t)comm_.nranks;
     u1_ = U.m * (uint64_t)(comm_.rank + 1) / (uint64_t)comm_.nranks;
@@ -398,11 +408,14 @@ template <typename real> class Problem final : public ProblemBase {
     std::memset(run_host_, 0, sizeof(int) * (MAXCG + 2));
     HIPCHK(hipHostGetDevicePointer((void **)&run_host_dev_, run_host_, 0));
     if (comm_.host_fn) HIPCHK(hipHostMalloc((void **)&stage_, Dmax * kp_ * sizeof(real), hipHostMallocDefault));
+    if (comm_.host_fn) HIPCHK(hipHostMalloc((void **)&dstage_, DSTAGE * sizeof(double), hipHostMallocDefault));
+    dots_.alloc(4);
   }
 
   ~Problem() override {
     if (run_host_) (void)hipHostFree(run_host_);
     if (stage_) (void)hipHostFree(stage_);
+    if (dstage_) (void)hipHostFree(dstage_);
     for (auto &e : ev_pool_) (void)hipEventDestroy(e);
     if (stream_) (void)hipStreamDestroy(stream_);
     if (comm_.nccl) ncclCommDestroy(comm_.nccl);
@@ -507,6 +520,7 @@ template <typename real> class Problem final : public ProblemBase {
   // ------------------------------------------------------- validation
   void validate(ocffm_metrics *out) override {
     need_init();
+    sync_owned();
     static const uint32_t cuts[5] = {5, 10, 20, 40, 80};
     for (int s = 0; s < 5; s++) out->top_k[s] = cuts[s];
     if (!has_test_) {
@@ -587,6 +601,7 @@ template <typename real> class Problem final : public ProblemBase {
     switch (what) {
       case 'W': case 'H': case 'P': case 'Q': {
         if (b12 >= blocks_.size() || !blocks_[b12].used) throw Error(OCFFM_E_ARG, "block not in the model");
+        if (what == 'W' || what == 'H') sync_owned();
         const Block &b = blocks_[b12];
         cols = k_;
         if (what == 'W') { src = W_[b12].p; rows = side(b.f1).Ds[fidx(b.f1)]; }
@@ -720,8 +735,29 @@ template <typename real> class Problem final : public ProblemBase {
 
  private:
   // ------------------------------------------------------------ setup
+  // Owned field test over the contiguous row shards of all ranks (every rank
+  // holds the whole HostData, so no communication is needed).
+  void ownership(DevField<real> &F, const HostData &d, uint64_t fi) {
+    const uint64_t m = d.m, N = (uint64_t)comm_.nranks;
+    std::vector<int32_t> who(F.D, -1);
+    bool excl = true;
+    for (uint64_t q = 0; q < N && excl; q++) {
+      const uint64_t a = m * q / N, b = m * (q + 1) / N;
+      for (int64_t p = d.xptr[fi][a]; p < d.xptr[fi][b] && excl; p++) {
+        int32_t &w = who[d.xidx[fi][p]];
+        if (w < 0) w = (int32_t)q;
+        else if (w != (int32_t)q) excl = false;
+      }
+    }
+    if (!excl || no_owned_) return;
+    F.excl = true;
+    F.h_own.resize(F.D);
+    for (uint64_t x = 0; x < F.D; x++) F.h_own[x] = who[x] == comm_.rank || (who[x] < 0 && comm_.rank == 0);
+    F.own.upload(F.h_own);
+  }
+
   void build_fields(DevSide<real> &s, const HostData &d, uint64_t r0, uint64_t r1,
-                    const std::vector<uint64_t> &Ds_glob) {
+                    const std::vector<uint64_t> &Ds_glob, bool owned = false) {
     s.F.clear();
     s.Ds = Ds_glob;
     const uint64_t R = r1 - r0;
@@ -749,13 +785,15 @@ template <typename real> class Problem final : public ProblemBase {
         }
         F->idlike = ok;
       }
+      if (owned && fi < d.f) ownership(*F, d, fi);
       F->xptr.upload(xptr);
       F->xidx.upload(xidx);
       F->xval.upload(to_real(xval));
       std::vector<uint32_t> crow;
       std::vector<double> cval;
       std::vector<Job> jobs;
-      build_csc(R, F->D, xptr.data(), xidx.data(), xval.data(), nsg(), crow, cval, jobs, F->nslot);
+      build_csc(R, F->D, xptr.data(), xidx.data(), xval.data(), nsg(), crow, cval, jobs, F->nslot,
+                F->excl ? F->h_own.data() : nullptr);
       F->crow.upload(crow);
       F->cval.upload(to_real(cval));
       F->jobs.upload(jobs);
@@ -777,7 +815,7 @@ template <typename real> class Problem final : public ProblemBase {
     U_.R = u1_ - u0_;
     U_.R_glob = U.m;
     U_.row0 = u0_;
-    build_fields(U_, U, u0_, u1_, U.Ds);
+    build_fields(U_, U, u0_, u1_, U.Ds, comm_.nranks > 1);
     const uint64_t pb = U.yptr[u0_], pe = U.yptr[u1_];
     std::vector<int64_t> yptr(U_.R + 1);
     for (uint64_t i = 0; i <= U_.R; i++) yptr[i] = (int64_t)(U.yptr[u0_ + i] - pb);
@@ -1067,6 +1105,46 @@ template <typename real> class Problem final : public ProblemBase {
     }
   }
 
+  void allreduce_dev_d(double *buf, uint64_t count) {
+    if (!comm_.active()) return;
+    if (comm_.nccl) {
+      NCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, comm_.nccl, stream_));
+    } else {
+      if (count > DSTAGE) throw Error(OCFFM_E_ARG, "allreduce_dev_d: too many values");
+      HIPCHK(hipMemcpyAsync(dstage_, buf, count * sizeof(double), hipMemcpyDeviceToHost, stream_));
+      sync();
+      if (comm_.host_fn(dstage_, count, 1, comm_.host_user) != 0)
+        throw Error(OCFFM_E_COMM, "host all-reduce callback failed");
+      HIPCHK(hipMemcpyAsync(buf, dstage_, count * sizeof(double), hipMemcpyHostToDevice, stream_));
+    }
+  }
+
+  // Make the owned fields' tables whole on every rank (each rank keeps only
+  // its own feature rows current): zero the others, sum over the ranks.
+  void sync_owned() {
+    if (!owned_stale_) return;
+    owned_stale_ = false;
+    for (uint32_t f1 = 0; f1 < f_; f1++)
+      for (uint32_t f2 = f1; f2 < f_; f2++) {
+        const uint32_t b12 = block_index(f1, f2, f_);
+        if (!blocks_[b12].used) continue;
+        for (int t = 0; t < 2; t++) {
+          const uint32_t fl = t == 0 ? f1 : f2;
+          DevField<real> &F = *side(fl).F[fidx(fl)];
+          if (!F.excl) continue;
+          real *T = t == 0 ? W_[b12].p : H_[b12].p;
+          with_kp(kp_, [&](auto K) {
+            constexpr int KP = decltype(K)::value;
+            using Gm = Geo<real, KP>;
+            const uint64_t nv = F.D * KP / Gm::VE;
+            launch(k_mask_rows<real>, grid_for(nv, BLOCK, 2048), BLOCK, 0, nv, T, F.own.p, (uint32_t)Gm::LPR);
+          });
+          allreduce_dev(T, F.D * kp_);
+        }
+      }
+    sync();
+  }
+
   void allreduce_host(double *buf, uint64_t count) {
     if (!comm_.active()) return;
     if (comm_.nccl) {
@@ -1212,6 +1290,7 @@ template <typename real> class Problem final : public ProblemBase {
     f.tick = tick_.p;
     f.run_host = run_host_dev_;
     f.it = it;
+    f.dots = h.F->excl ? dots_.p : nullptr;
     return f;
   }
   // id-like field on one GPU: the row pass finalises its feature column.
@@ -1258,6 +1337,17 @@ template <typename real> class Problem final : public ProblemBase {
   void feature_pass(HalfCtx &h, int it, bool seg) {
     if (!comm_.active()) {
       feat_launch(h, it, seg, it == 0 ? 0 : 1);
+      return;
+    }
+    if (h.F->excl) {  // owned field: local columns only, then the dot products meet
+      if (!(seg ? h.F->snjw : h.F->njw)) HIPCHK(hipMemsetAsync(dots_.p, 0, 3 * sizeof(double), stream_));
+      else feat_launch(h, it, seg, it == 0 ? 0 : 1);
+      allreduce_dev_d(dots_.p, 3);
+      const Fin<real> fin = make_fin(h, it);
+      prof_launch("cg_step", 0, [&] {
+        if (it == 0) launch(k_cg_step<real, 0>, 1, 64, 0, fin);
+        else launch(k_cg_step<real, 1>, 1, 64, 0, fin);
+      });
       return;
     }
     scatter(h, it, seg);
@@ -1376,8 +1466,11 @@ template <typename real> class Problem final : public ProblemBase {
       using Gm = Geo<real, KP>;
       const double rs = sizeof(real);
       const uint64_t nv = h.D * KP / Gm::VE;
+      const bool excl = h.F->excl;
+      if (excl) owned_stale_ = true;
       prof_launch("apply_step", (double)h.D * KP * rs * 5, [&] {
-        launch(k_apply<real>, grid_for(nv, BLOCK, 2048), BLOCK, 0, nv, Vd_.p, S_.p, h.W1, st_.p);
+        launch(k_apply<real>, grid_for(nv, BLOCK, 2048), BLOCK, 0, nv, Vd_.p, S_.p, h.W1, st_.p,
+               excl ? (const uint8_t *)h.F->own.p : nullptr, (uint32_t)Gm::LPR);
       });
       if (own.R == 0) return;
       DevField<real> &F = *h.F;
@@ -1446,6 +1539,8 @@ template <typename real> class Problem final : public ProblemBase {
   uint64_t seg_len_ = 32;
   int lookahead_ = 1;
   bool no_fuse_ = true;
+  bool no_owned_ = false;
+  bool owned_stale_ = false;  // owned tables differ across ranks until sync_owned()
   unsigned hs_blocks_ = 4096;  // grid cap of the cross Hessian-vector row pass
   hipEvent_t arm_a_ = nullptr, arm_b_ = nullptr;
   bool arm_first_ = false;
@@ -1460,6 +1555,9 @@ template <typename real> class Problem final : public ProblemBase {
   DevBuf<real *> tabs_;
   int *run_host_ = nullptr, *run_host_dev_ = nullptr;
   real *stage_ = nullptr;
+  static constexpr uint64_t DSTAGE = 64;
+  double *dstage_ = nullptr;  // host all-reduce stage of the owned-field dot products
+  DevBuf<double> dots_;
   struct Pending {
     std::string name;
     double bytes;

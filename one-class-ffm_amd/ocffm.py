@@ -259,6 +259,10 @@ class ImpProblem:
     def __del__(self):
         self.close()
 
+    def n_blocks(self) -> int:
+        """Field-pair blocks f(f+1)/2 (ffm.cpp:53-55); unused ones (--ns) included."""
+        return self.f * (self.f + 1) // 2
+
     def init(self):
         _check(lib().ocffm_problem_init(self.h))
 

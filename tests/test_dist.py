@@ -156,7 +156,15 @@ def test_sharded_decomposition_gloo():
 
 
 # ------------------------------------------------------------------ GPU ---
-def _gpu_worker(rank, port, out_dir, world):
+def _dist_dataset(name):
+    if name == "tiny":
+        return synth.tiny(seed=8)
+    # a listener-id field (D = m): every feature belongs to one rank's rows,
+    # so its CG vectors stay sharded and only dot products are summed
+    return synth.kkbox(seed=5, m=300, n=400, mean=12.0, name="kkbox_dist")
+
+
+def _gpu_worker(rank, port, out_dir, world, name="tiny"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import ocffm
@@ -165,37 +173,44 @@ def _gpu_worker(rank, port, out_dir, world):
         t = torch.from_numpy(arr)
         dist.all_reduce(t)
 
-    ds = synth.tiny(seed=8)
+    ds = _dist_dataset(name)
     g = ocffm.problem_from_dataset(ds, precision=ocffm.FP64, rank=rank, nranks=world, allreduce=allreduce)
     ocffm.srand(1)
     g.init()
+    g.set_profiling(True)
     for _ in range(2):
         g.one_epoch()
+    steps = g.kernel_stats().get("cg_step", {}).get("launches", 0)
     met = g.validate()
-    W = [g.get("W", b) for b in range(6)] + [g.get("H", b) for b in range(6)]
+    nb = g.n_blocks()
+    W = [g.get("W", b) for b in range(nb)] + [g.get("H", b) for b in range(nb)]
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), cg=g.cg_log(), loss=met["loss"], ndcg=met["ndcg"],
-             prec=met["prec"], *W)
+             prec=met["prec"], steps=steps, *W)
     g.close()
     dist.destroy_process_group()
 
 
 @pytest.mark.gpu
-def test_two_ranks_match_one_rank_on_gpu():
+@pytest.mark.parametrize("name", ["tiny", "owned"])
+def test_two_ranks_match_one_rank_on_gpu(name):
     import ocffm
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_gpu_worker, args=(_free_port(), d, WORLD), nprocs=WORLD, join=True)
+        mp.spawn(_gpu_worker, args=(_free_port(), d, WORLD, name), nprocs=WORLD, join=True)
         r0 = np.load(os.path.join(d, "r0.npz"))
         r1 = np.load(os.path.join(d, "r1.npz"))
-        ds = synth.tiny(seed=8)
+        ds = _dist_dataset(name)
         g = ocffm.problem_from_dataset(ds, precision=ocffm.FP64)
         ocffm.srand(1)
         g.init()
         for _ in range(2):
             g.one_epoch()
         met = g.validate()
+        nb = g.n_blocks()
+        # the owned-field path ran (listener-id halves) only where it applies
+        assert (int(r0["steps"]) > 0) == (name == "owned")
         np.testing.assert_array_equal(r0["cg"], g.cg_log())
         np.testing.assert_array_equal(r1["cg"], g.cg_log())
-        for idx, (what, b) in enumerate([("W", b) for b in range(6)] + [("H", b) for b in range(6)]):
+        for idx, (what, b) in enumerate([("W", b) for b in range(nb)] + [("H", b) for b in range(nb)]):
             ref = g.get(what, b)
             for r in (r0, r1):
                 x = r[f"arr_{idx}"]

@@ -88,6 +88,14 @@ int ocffm_data_trans_y(ocffm_data *V, const ocffm_data *U);
 int ocffm_data_get_info(const ocffm_data *d, ocffm_data_info *out);
 /* Per-field Ds (ffm.cpp:221); out must hold info.f values. */
 int ocffm_data_get_ds(const ocffm_data *d, uint64_t *out);
+/* The parsed labels (ffm.cpp:93-101: U->Y before transY): yptr holds info.m+1
+ * offsets, ycol info.nnz_y item indices.  Either pointer may be NULL. */
+int ocffm_data_get_labels(const ocffm_data *d, uint64_t *yptr, uint64_t *ycol);
+/* One field's CSR after split_fields (ffm.cpp:185-257): xptr info.m+1
+ * offsets, then that field's node indices and values.  Pointers may be NULL;
+ * *nnz receives the field's node count. */
+int ocffm_data_get_field(const ocffm_data *d, uint32_t field, int64_t *xptr, uint32_t *xidx, double *xval,
+                         uint64_t *nnz);
 void ocffm_data_free(ocffm_data *d);
 
 /* --------------------------------------------------------------- problem

@@ -7,8 +7,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <random>
 #include <stdexcept>
+#include <string>
+#include <thread>
 
 namespace ocffm {
 
@@ -78,26 +81,53 @@ inline uint64_t parse_label(const char *b, const char *e) {
 
 }  // namespace
 
-// ffm.cpp:80-183 in one pass: label block, then fid:idx:val triples until the
-// first token that does not parse; an empty line re-uses the previous label
-// block (the stale label_block of ffm.cpp:93).
-Rows parse_rows(const std::string &path, bool has_label, const uint64_t *ds, uint64_t nds) {
-  FILE *fp = std::fopen(path.c_str(), "rb");
-  if (!fp) throw std::runtime_error("cannot open " + path);
-  std::fseek(fp, 0, SEEK_END);
-  long sz = std::ftell(fp);
-  std::fseek(fp, 0, SEEK_SET);
-  std::string buf((size_t)std::max(0L, sz), '\0');
-  if (sz > 0 && std::fread(&buf[0], 1, (size_t)sz, fp) != (size_t)sz) {
-    std::fclose(fp);
-    throw std::runtime_error("read failed: " + path);
-  }
-  std::fclose(fp);
-
+// One chunk of a file (whole lines) parsed by one thread.  Blank lines at
+// the chunk start re-use the label block of an earlier chunk: they are
+// counted (lead_blank) and resolved when the chunks are joined in order.
+struct Chunk {
   Rows r;
+  uint64_t lead_blank = 0;
+  bool any_label = false;   // a non-blank line set the label block
+  std::string last_block;   // the label block in force at the chunk end
+  std::exception_ptr err;
+};
+
+static void parse_labels(const std::string &block, std::vector<uint64_t> &ycol, uint64_t &n) {
+  const char *lb = block.data(), *le = lb + block.size();
+  while (lb < le) {
+    const char *c = (const char *)std::memchr(lb, ',', (size_t)(le - lb));
+    if (!c) c = le;
+    const uint64_t j = parse_label(lb, c);
+    ycol.push_back(j);
+    n = std::max(n, j + 1);
+    lb = c + 1;
+  }
+}
+
+// ffm.cpp:80-183 on the lines [s, end): label block, then fid:idx:val
+// triples until the first token that does not parse; an empty line re-uses
+// the previous label block (the stale label_block of ffm.cpp:93).
+static void parse_chunk(const char *s, const char *end, bool has_label, const uint64_t *ds, uint64_t nds, Chunk &ck,
+                        bool reserve) {
+  Rows &r = ck.r;
   r.has_label = has_label;
-  std::string label_block;
-  const char *s = buf.data(), *end = s + buf.size();
+  // Parallel chunks reserve from the chunk size (a label takes >= 2 bytes, a
+  // node >= 6): growing vectors in parallel threads re-map memory, and every
+  // unmap in a threaded process stalls all of its threads (TLB shootdowns).
+  if (reserve) {
+    const size_t bytes = (size_t)(end - s);
+    size_t lines = 1;
+    for (const char *q = s; (q = (const char *)std::memchr(q, '\n', (size_t)(end - q))) != nullptr; q++) lines++;
+    r.xptr.reserve(lines + 1);
+    if (has_label) {
+      r.yptr.reserve(lines + 1);
+      r.ycol.reserve(bytes / 2 + 1);
+    }
+    r.fid.reserve(bytes / 6 + 1);
+    r.idx.reserve(bytes / 6 + 1);
+    r.val.reserve(bytes / 6 + 1);
+  }
+  std::string &label_block = ck.last_block;
   while (s < end) {
     const char *e = (const char *)std::memchr(s, '\n', (size_t)(end - s));
     if (!e) e = end;
@@ -108,17 +138,11 @@ Rows parse_rows(const std::string &path, bool has_label, const uint64_t *ds, uin
         const char *q = p;
         while (q < e && !std::isspace((unsigned char)*q)) q++;
         label_block.assign(p, q);
+        ck.any_label = true;
         p = q;
       }
-      const char *lb = label_block.data(), *le = lb + label_block.size();
-      while (lb < le) {
-        const char *c = (const char *)std::memchr(lb, ',', (size_t)(le - lb));
-        if (!c) c = le;
-        uint64_t j = parse_label(lb, c);
-        r.ycol.push_back(j);
-        r.n = std::max(r.n, j + 1);
-        lb = c + 1;
-      }
+      if (!ck.any_label) ck.lead_blank++;  // labels resolved at the join
+      else parse_labels(label_block, r.ycol, r.n);
       r.yptr.push_back(r.ycol.size());
     }
     while (true) {
@@ -135,6 +159,96 @@ Rows parse_rows(const std::string &path, bool has_label, const uint64_t *ds, uin
     }
     r.xptr.push_back(r.fid.size());
     s = e + 1;
+  }
+}
+
+// The whole file in memory, cut into line-aligned chunks parsed by parallel
+// threads (files under 4 MB: one), joined in file order.
+Rows parse_rows(const std::string &path, bool has_label, const uint64_t *ds, uint64_t nds) {
+  FILE *fp = std::fopen(path.c_str(), "rb");
+  if (!fp) throw std::runtime_error("cannot open " + path);
+  std::fseek(fp, 0, SEEK_END);
+  long sz = std::ftell(fp);
+  std::fseek(fp, 0, SEEK_SET);
+  std::string buf((size_t)std::max(0L, sz), '\0');
+  if (sz > 0 && std::fread(&buf[0], 1, (size_t)sz, fp) != (size_t)sz) {
+    std::fclose(fp);
+    throw std::runtime_error("read failed: " + path);
+  }
+  std::fclose(fp);
+
+  const char *b = buf.data(), *end = b + buf.size();
+  const unsigned hw = std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
+  unsigned nth = buf.size() < (4u << 20) ? 1u : hw;
+  if (const char *e = std::getenv("OCFFM_PARSE_CHUNKS")) nth = (unsigned)std::max(1, std::atoi(e));  // tests
+  std::vector<const char *> cut{b};
+  for (unsigned t = 1; t < nth; t++) {
+    const char *c = std::max(cut.back(), b + buf.size() * t / nth);
+    const char *nl = c < end ? (const char *)std::memchr(c, '\n', (size_t)(end - c)) : nullptr;
+    cut.push_back(nl ? nl + 1 : end);
+  }
+  cut.push_back(end);
+  std::vector<Chunk> ck(nth);
+  auto work = [&](unsigned t) {
+    try {
+      parse_chunk(cut[t], cut[t + 1], has_label, ds, nds, ck[t], nth > 1);
+    } catch (...) {
+      ck[t].err = std::current_exception();
+    }
+  };
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < nth; t++) th.emplace_back(work, t);
+  work(0);
+  for (auto &x : th) x.join();
+
+  // join in file order; the first error in file order wins, as in a serial read
+  Rows r;
+  r.has_label = has_label;
+  if (nth == 1 && !ck[0].err && !ck[0].lead_blank) return std::move(ck[0].r);
+  size_t nx = 0, ny = 0, nr = 0;
+  for (auto &c : ck) {
+    nx += c.r.fid.size();
+    ny += c.r.ycol.size();
+    nr += c.r.xptr.size();
+  }
+  r.fid.reserve(nx);
+  r.idx.reserve(nx);
+  r.val.reserve(nx);
+  r.xptr.reserve(nr);
+  if (has_label) {
+    r.yptr.reserve(nr);
+    r.ycol.reserve(ny + 1024);
+  }
+  std::string carried;  // label block in force before the chunk
+  for (unsigned t = 0; t < nth; t++) {
+    Chunk &c = ck[t];
+    std::vector<uint64_t> inherited;
+    if (has_label && c.lead_blank) {
+      try {
+        parse_labels(carried, inherited, r.n);
+      } catch (...) {
+        std::rethrow_exception(std::current_exception());
+      }
+    }
+    if (c.err) std::rethrow_exception(c.err);
+    const uint64_t x0 = r.fid.size();
+    r.fid.insert(r.fid.end(), c.r.fid.begin(), c.r.fid.end());
+    r.idx.insert(r.idx.end(), c.r.idx.begin(), c.r.idx.end());
+    r.val.insert(r.val.end(), c.r.val.begin(), c.r.val.end());
+    for (size_t i = 1; i < c.r.xptr.size(); i++) r.xptr.push_back(x0 + c.r.xptr[i]);
+    if (has_label) {
+      uint64_t y0 = r.ycol.size();
+      for (uint64_t i = 0; i < c.lead_blank; i++) {
+        r.ycol.insert(r.ycol.end(), inherited.begin(), inherited.end());
+        r.yptr.push_back(r.ycol.size());
+      }
+      y0 = r.ycol.size();
+      r.ycol.insert(r.ycol.end(), c.r.ycol.begin(), c.r.ycol.end());
+      for (size_t i = 1 + c.lead_blank; i < c.r.yptr.size(); i++) r.yptr.push_back(y0 + c.r.yptr[i]);
+      if (c.any_label) carried = c.last_block;
+    }
+    r.f = std::max(r.f, c.r.f);
+    r.n = std::max(r.n, c.r.n);
   }
   return r;
 }
@@ -210,12 +324,39 @@ static double qrsqrt(double x) {
   return x * (1.5 - half * x * x);
 }
 
+// The table's one engine is consumed in order; every double takes exactly
+// two engine steps (generate_canonical<double, 53> over minstd_rand0's
+// 31-bit range), so the stream is cut into chunks whose start state is the
+// seed state times a^(2*start) mod m (LCG jump-ahead) and the chunks are
+// drawn by parallel threads through the same distribution object code: the
+// values are those of one serial pass.
+static uint64_t mulmod(uint64_t a, uint64_t b, uint64_t m) { return (uint64_t)((unsigned __int128)a * b % m); }
+static uint64_t powmod(uint64_t a, uint64_t e, uint64_t m) {
+  uint64_t r = 1;
+  for (a %= m; e; e >>= 1, a = mulmod(a, a, m))
+    if (e & 1) r = mulmod(r, a, m);
+  return r;
+}
+
 void init_table(double *out, uint64_t rows, uint32_t cols) {
-  std::minstd_rand0 eng(std::rand());
+  using E = std::minstd_rand0;
+  const uint64_t seed = (uint64_t)(unsigned)std::rand();
   const double b = 0.1 * qrsqrt((double)cols);
-  std::uniform_real_distribution<double> dist(-b, b);
   const uint64_t nn = rows * cols;
-  for (uint64_t i = 0; i < nn; i++) out[i] = dist(eng);
+  uint64_t x0 = seed % E::modulus;
+  if (x0 == 0) x0 = 1;  // linear_congruential_engine::seed
+  const unsigned hw = std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
+  const unsigned nth = nn < (1u << 16) ? 1u : hw;
+  auto work = [&](unsigned t) {
+    const uint64_t i0 = nn * t / nth, i1 = nn * (t + 1) / nth;
+    E eng((E::result_type)mulmod(x0, powmod(E::multiplier, 2 * i0, E::modulus), E::modulus));
+    std::uniform_real_distribution<double> dist(-b, b);
+    for (uint64_t i = i0; i < i1; i++) out[i] = dist(eng);
+  };
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < nth; t++) th.emplace_back(work, t);
+  work(0);
+  for (auto &x : th) x.join();
 }
 
 }  // namespace ocffm

@@ -1280,13 +1280,14 @@ __global__ __launch_bounds__(BLOCK) void k_gram_part(uint64_t Rp, int L, const r
   }
 }
 
-// out[o - off] = sum_b part[b][o] for o in [off, off + cnt): a block owns 16
-// consecutive outputs (coalesced 128-B reads) and 16 groups of partial rows;
-// groups are combined in fixed order through LDS (deterministic).
+// o in [0, cnt): t = sum_b part[b][off + o]; o < split -> out_real[o] = t,
+// else out_dbl[o - split] = t.  A block owns 16 consecutive outputs
+// (coalesced 128-B reads) and 16 groups of partial rows; groups are combined
+// in fixed order through LDS (deterministic).
 template <typename real>
 __global__ __launch_bounds__(BLOCK) void k_reduce_parts(uint64_t nb, uint64_t nout, uint64_t off, uint64_t cnt,
-                                                        const double *__restrict__ part, double *__restrict__ out,
-                                                        real *__restrict__ out_real) {
+                                                        const double *__restrict__ part, uint64_t split,
+                                                        real *__restrict__ out_real, double *__restrict__ out_dbl) {
   __shared__ double sh[16][17];
   const int to = threadIdx.x & 15, tg = threadIdx.x >> 4;
   const uint64_t o = (uint64_t)blockIdx.x * 16 + to;
@@ -1306,8 +1307,51 @@ __global__ __launch_bounds__(BLOCK) void k_reduce_parts(uint64_t nb, uint64_t no
     double t = 0;
 #pragma unroll
     for (int g = 0; g < 16; g++) t += sh[g][to];
-    if (out) out[o] = t;
-    if (out_real) out_real[o] = (real)t;
+    if (o < split) out_real[o] = (real)t;
+    else out_dbl[o - split] = t;
+  }
+}
+
+// Column sums of C tables at once (cache_sasb, ffm.cpp:514-535):
+// part[block][c*KP + d] = sum over the block's rows j of T_c[j][d].  Rows are
+// read 16 B per lane, BLOCK/LPR rows per pass; row groups are combined in
+// fixed order through LDS (deterministic); k_reduce_parts sums the blocks.
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_colsum_multi(uint64_t R, int C, const real *const *__restrict__ tabs,
+                                                        double *__restrict__ part, uint64_t rows_per_block) {
+  using G = Geo<real, KP>;
+  constexpr int RG = BLOCK / G::LPR;  // row groups per pass
+  __shared__ double sh[RG][KP + 1];
+  const int li = threadIdx.x % G::LPR, rg = threadIdx.x / G::LPR;
+  const uint64_t r0 = (uint64_t)blockIdx.x * rows_per_block;
+  const uint64_t r1 = min(R, r0 + rows_per_block);
+  for (int c = 0; c < C; c++) {
+    const real *T = tabs[c];
+    double a[G::VE];
+#pragma unroll
+    for (int e = 0; e < G::VE; e++) a[e] = 0;
+    uint64_t j = r0 + rg;
+    for (; j + 3 * RG < r1; j += 4 * RG) {
+      const vec_t<real> x0 = vld<real>(T + j * KP + li * G::VE), x1 = vld<real>(T + (j + RG) * KP + li * G::VE);
+      const vec_t<real> x2 = vld<real>(T + (j + 2 * RG) * KP + li * G::VE);
+      const vec_t<real> x3 = vld<real>(T + (j + 3 * RG) * KP + li * G::VE);
+#pragma unroll
+      for (int e = 0; e < G::VE; e++) a[e] += ((double)x0[e] + (double)x1[e]) + ((double)x2[e] + (double)x3[e]);
+    }
+    for (; j < r1; j += RG) {
+      const vec_t<real> x = vld<real>(T + j * KP + li * G::VE);
+#pragma unroll
+      for (int e = 0; e < G::VE; e++) a[e] += (double)x[e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < G::VE; e++) sh[rg][li * G::VE + e] = a[e];
+    __syncthreads();
+    if (threadIdx.x < KP) {
+      double t = 0;
+      for (int g = 0; g < RG; g++) t += sh[g][threadIdx.x];
+      part[(uint64_t)blockIdx.x * C * KP + (uint64_t)c * KP + threadIdx.x] = t;
+    }
   }
 }
 

@@ -12,6 +12,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <charconv>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -24,6 +25,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -352,14 +354,18 @@ template <typename real> class Problem final : public ProblemBase {
     if (const char *e = std::getenv("OCFFM_SEG_LEN")) seg_len_ = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
     if (const char *e = std::getenv("OCFFM_LOOKAHEAD")) lookahead_ = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("OCFFM_HS_BLOCKS")) hs_blocks_ = (unsigned)std::max(1, std::atoi(e));
-    if (const char *e = std::getenv("OCFFM_FUSE")) no_fuse_ = std::atoi(e) == 0;  // id-field row fusion: opt-in
+    if (const char *e = std::getenv("OCFFM_FUSE")) fuse_ = std::atoi(e);  // id-field row fusion: 0 off, 1 side, 2 all
     if (const char *e = std::getenv("OCFFM_NO_OWNED")) no_owned_ = std::atoi(e) != 0;  // all-reduce every field
     // shard users contiguously
     u0_ = U.m * (uint64_t)comm_.rank / (uint64_t)comm_.nranks;
     u1_ = U.m * (uint64_t)(comm_.rank + 1) / (uint64_t)comm_.nranks;
+    tmark(nullptr);
     build_user_side(U);
+    tmark("create: user side");
     build_item_side(V, U);
+    tmark("create: item side");
     if (Ut) build_test(*Ut, U);
+    tmark("create: test rows");
     popular_.upload(U.popular);
     npop_ = U.popular.size();
     blocks_.resize(f_ * (f_ + 1) / 2);
@@ -398,7 +404,6 @@ template <typename real> class Problem final : public ProblemBase {
     tick_.alloc(TICK_WORDS);
     C_ = fu_ * fv_;
     M_.alloc(std::max<uint32_t>(C_, 1) * kp_ * kp_);
-    QTQ_.alloc((size_t)kp_ * kp_);
     sums_.alloc(2 * kp_ + 1);
     vecs_.alloc((size_t)std::max<uint32_t>(C_, 1) * kp_);
     part_.alloc(1 << 22, false);
@@ -428,7 +433,21 @@ template <typename real> class Problem final : public ProblemBase {
 
   // --------------------------------------------------------------- init
   // ffm.cpp:467-512.
+  // OCFFM_TIMING=1: host wall time of set-up phases on stderr.
+  void tmark(const char *name) {
+    static const bool on = std::getenv("OCFFM_TIMING") != nullptr;
+    if (!on) return;
+    if (name) {
+      HIPCHK(hipStreamSynchronize(stream_));
+      std::fprintf(stderr, "[timing]   %-22s %9.3f ms\n", name,
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tmark_t_).count());
+    }
+    tmark_t_ = std::chrono::steady_clock::now();
+  }
+  std::chrono::steady_clock::time_point tmark_t_;
+
   void init() override {
+    tmark(nullptr);
     const size_t rs = sizeof(real);
     std::vector<double> host;
     for (uint32_t f1 = 0; f1 < f_; f1++)
@@ -459,9 +478,12 @@ template <typename real> class Problem final : public ProblemBase {
         tl[C_ + c] = Q_[b12].p;       // item-side cross tables
       }
     HIPCHK(hipMemcpy(tabs_.p, tl.data(), tl.size() * sizeof(real *), hipMemcpyHostToDevice));
+    tmark("init: tables + UTX");
     cache_sasb();
     if (prm_.self_side) calc_side();
+    tmark("init: sasb + side");
     init_y_tilde();
+    tmark("init: y~");
     sync();
     inited_ = true;
   }
@@ -499,14 +521,22 @@ template <typename real> class Problem final : public ProblemBase {
     for (int sidew = 0; sidew < 2; sidew++) {
       DevSide<real> &part_side = sidew == 0 ? V_ : U_;   // rows summed
       DevSide<real> &out_side = sidew == 0 ? U_ : V_;    // rows scored
-      for (uint32_t c = 0; c < C_; c++) {
-        real *tab = cross_tab(sidew == 0 ? 1 : 0, c);
-        aggregates(part_side.R, 0, nullptr, tab, nullptr, nullptr);
-        HIPCHK(hipMemcpyAsync(vecs_.p + (size_t)c * kp_, sums_.p, kp_ * sizeof(double), hipMemcpyDeviceToDevice, stream_));
-      }
       with_kp(kp_, [&](auto K) {
         constexpr int KP = decltype(K)::value;
         using Gm = Geo<real, KP>;
+        // column sums of every cross table of the summed side -> vecs_ (C x KP doubles)
+        const uint64_t Rs = part_side.R, nout = (uint64_t)C_ * KP;
+        uint64_t nbx = std::max<uint64_t>(1, std::min<uint64_t>((Rs + 255) / 256, 512));
+        nbx = std::min<uint64_t>(nbx, std::max<uint64_t>(1, part_.n / nout));
+        const uint64_t rpb = (Rs + nbx - 1) / nbx;
+        prof_launch("aggregates", (double)Rs * C_ * KP * sizeof(real), [&] {
+          launch(k_colsum_multi<real, KP>, (unsigned)nbx, BLOCK, 0, Rs, (int)C_,
+                 (const real *const *)(tabs_.p + (sidew == 0 ? C_ : 0)), part_.p, rpb);
+        });
+        prof_launch("aggr_reduce", (double)nbx * nout * 8, [&] {
+          launch(k_reduce_parts<real>, (unsigned)((nout + 15) / 16), BLOCK, 0, nbx, nout, (uint64_t)0, nout, part_.p,
+                 (uint64_t)0, (real *)nullptr, vecs_.p);
+        });
         const uint64_t R = out_side.R;
         if (R == 0) return;
         prof_launch("rowdot_multi", (double)R * (C_ * kp_ * sizeof(real) + sizeof(real)), [&] {
@@ -691,8 +721,7 @@ template <typename real> class Problem final : public ProblemBase {
     if (hc.cross) {  // QTQ over the partner rows (slot of this block in the Gram list)
       aggregates(hc.partner->R, (int)C_, partner_tabs(hc), hc.Q1, nullptr, M_.p);
       const uint32_t c0 = cross_slot(std::min(hc.fl, hc.fo), std::max(hc.fl, hc.fo));
-      HIPCHK(hipMemcpyAsync(QTQ_.p, M_.p + (size_t)c0 * kp_ * kp_, (size_t)kp_ * kp_ * sizeof(real),
-                            hipMemcpyDeviceToDevice, stream_));
+      qtq_ = M_.p + (size_t)c0 * kp_ * kp_;
     }
     // force iteration 1 to run
     CgState hs{};
@@ -705,32 +734,60 @@ template <typename real> class Problem final : public ProblemBase {
     copy_out(Hv_.p, hc.D, out);
   }
 
-  // ffm.cpp:1163-1237: the reference's text model.
+  // ffm.cpp:1163-1237: the reference's text model.  Values are formatted as
+  // the reference's ostream does by default (precision 6, %g), by
+  // std::to_chars(general, 6), which the standard defines as that printf
+  // conversion; row ranges are formatted by parallel host threads and
+  // written in order.
   void save_model(const std::string &path) override {
     need_init();
-    std::ofstream o(path, std::ios::out | std::ios::trunc);
-    if (!o) throw Error(OCFFM_E_IO, "cannot write " + path);
-    o << f_ << "\n" << fu_ << "\n" << fv_ << "\n" << k_ << "\n";
-    for (uint32_t i = 0; i < fu_; i++) o << U_.Ds[i] << "\n";
-    for (uint32_t i = 0; i < fv_; i++) o << V_.Ds[i] << "\n";
+    std::FILE *fp = std::fopen(path.c_str(), "wb");
+    if (!fp) throw Error(OCFFM_E_IO, "cannot write " + path);
+    std::string head = std::to_string(f_) + "\n" + std::to_string(fu_) + "\n" + std::to_string(fv_) + "\n" +
+                       std::to_string(k_) + "\n";
+    for (uint32_t i = 0; i < fu_; i++) head += std::to_string(U_.Ds[i]) + "\n";
+    for (uint32_t i = 0; i < fv_; i++) head += std::to_string(V_.Ds[i]) + "\n";
+    bool ok = std::fwrite(head.data(), 1, head.size(), fp) == head.size();
+    const unsigned nth = std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
     std::vector<double> buf;
-    for (uint32_t fi = 0; fi < f_; fi++)
-      for (uint32_t fj = fi; fj < f_; fj++) {
+    std::vector<std::string> parts(nth);
+    for (uint32_t fi = 0; fi < f_ && ok; fi++)
+      for (uint32_t fj = fi; fj < f_ && ok; fj++) {
         const uint32_t b12 = block_index(fi, fj, f_);
         if (!blocks_[b12].used) continue;
-        for (int t = 0; t < 2; t++) {
+        for (int t = 0; t < 2 && ok; t++) {
           const char c = t == 0 ? 'W' : 'H';
           const uint64_t cnt = get(c, b12, nullptr, 0);
           buf.resize(cnt);
           get(c, b12, buf.data(), cnt);
           const uint64_t rows = cnt / k_;
-          for (uint64_t rr = 0; rr < rows; rr++) {
-            o << c << ',' << fi << ',' << fj << ',' << rr;
-            for (uint32_t e = 0; e < k_; e++) o << " " << buf[rr * k_ + e];
-            o << "\n";
-          }
+          const std::string pre = std::string(1, c) + "," + std::to_string(fi) + "," + std::to_string(fj) + ",";
+          auto work = [&](unsigned w) {
+            std::string &o = parts[w];
+            o.clear();
+            const uint64_t r0 = rows * w / nth, r1 = rows * (w + 1) / nth;
+            char num[64];
+            for (uint64_t rr = r0; rr < r1; rr++) {
+              o += pre;
+              auto res = std::to_chars(num, num + sizeof(num), rr);
+              o.append(num, res.ptr);
+              for (uint32_t e = 0; e < k_; e++) {
+                o += ' ';
+                res = std::to_chars(num, num + sizeof(num), buf[rr * k_ + e], std::chars_format::general, 6);
+                o.append(num, res.ptr);
+              }
+              o += '\n';
+            }
+          };
+          std::vector<std::thread> th;
+          for (unsigned w = 1; w < nth; w++) th.emplace_back(work, w);
+          work(0);
+          for (auto &x : th) x.join();
+          for (auto &o : parts) ok = ok && std::fwrite(o.data(), 1, o.size(), fp) == o.size();
         }
       }
+    ok = (std::fclose(fp) == 0) && ok;
+    if (!ok) throw Error(OCFFM_E_IO, "write failed: " + path);
   }
 
  private:
@@ -1074,16 +1131,13 @@ template <typename real> class Problem final : public ProblemBase {
         launch(k_gram_part<real, KP, SPT>, dim3((unsigned)nbx, gy), BLOCK, smem, Rp, L, A, B, wv, part_.p,
                                                                                       rpb, sub_per_y);
       });
+      // one reduction launch over [grams -> M (real) | sums -> sums_ (double)]
       const uint64_t ng = (uint64_t)L * KP * KP;
-      if (ng && M)
-        prof_launch("aggr_reduce", (double)nbx * ng * 8, [&] {
-          launch(k_reduce_parts<real>, (unsigned)((ng + 15) / 16), BLOCK, 0, nbx, nout, 0, ng, part_.p, nullptr,
-                                                                                  M);
-        });
-      if (sums)
-        prof_launch("aggr_reduce", (double)nbx * (2 * KP + 1) * 8, [&] {
-          launch(k_reduce_parts<real>, (unsigned)((2 * KP + 1 + 15) / 16), BLOCK, 0,
-              nbx, nout, ng, 2 * KP + 1, part_.p, sums_.p, nullptr);
+      const uint64_t gm = M ? ng : 0, off = M ? 0 : ng, cnt = gm + (sums ? 2 * KP + 1 : 0);
+      if (cnt)
+        prof_launch("aggr_reduce", (double)nbx * cnt * 8, [&] {
+          launch(k_reduce_parts<real>, (unsigned)((cnt + 15) / 16), BLOCK, 0, nbx, nout, off, cnt, part_.p, gm, M,
+                 sums_.p);
         });
       HIPCHK(hipGetLastError());
     });
@@ -1234,10 +1288,9 @@ template <typename real> class Problem final : public ProblemBase {
             else go(std::false_type(), std::false_type());
           }
         });
-        // QTQ for CG = M of this block
+        // QTQ for CG = M of this block (M_ is not rewritten before the half ends)
         const uint32_t c0 = cross_slot(std::min(h.fl, h.fo), std::max(h.fl, h.fo));
-        HIPCHK(hipMemcpyAsync(QTQ_.p, M_.p + (size_t)c0 * KP * KP, (size_t)KP * KP * sizeof(real),
-                              hipMemcpyDeviceToDevice, stream_));
+        qtq_ = M_.p + (size_t)c0 * KP * KP;
       } else {
         DevSide<real> &other = h.user ? V_ : U_;  // sum of the other side's bias (b_sum, ffm.cpp:551)
         aggregates(other.R, 0, nullptr, nullptr, other.bias.p, nullptr);
@@ -1294,7 +1347,12 @@ template <typename real> class Problem final : public ProblemBase {
     return f;
   }
   // id-like field on one GPU: the row pass finalises its feature column.
-  bool fused_rows(const HalfCtx &h) const { return h.F->idlike && !comm_.active() && !no_fuse_; }
+  // fuse_ 1: side halves only (a row is one feature, no partial sums); 2: cross
+  // halves too (multi-segment rows meet through column atomics: slower on
+  // Pareto-headed items).
+  bool fused_rows(const HalfCtx &h) const {
+    return h.F->idlike && !comm_.active() && (fuse_ >= 2 || (fuse_ == 1 && !h.cross));
+  }
 
   void scatter(HalfCtx &h, int it, bool seg) {
     DevField<real> &F = *h.F;
@@ -1387,7 +1445,7 @@ template <typename real> class Problem final : public ProblemBase {
           auto go = [&](auto fz, auto ml) {
             constexpr bool FZ = decltype(fz)::value, ML = decltype(ml)::value;
             launch(k_hs_cross_seg<real, KP, ML, FZ>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : hs_blocks_), BLOCK, smem, own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p,
-                                                         own.ycol.p, h.Q1, (uint64_t)h.partner->R, QTQ_.p, w_, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
+                                                         own.ycol.p, h.Q1, (uint64_t)h.partner->R, qtq_, w_, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
                                                          F.segd.p, F.segx.p, fin);
           };
           prof_launch(fz_ ? "hs_cross_fused" : "hs_cross_row", bytes, [&] {
@@ -1538,7 +1596,7 @@ template <typename real> class Problem final : public ProblemBase {
   uint64_t m_glob_ = 0, n_ = 0, u0_ = 0, u1_ = 0, dmax_ = 0, npop_ = 0;
   uint64_t seg_len_ = 32;
   int lookahead_ = 1;
-  bool no_fuse_ = true;
+  int fuse_ = 1;
   bool no_owned_ = false;
   bool owned_stale_ = false;  // owned tables differ across ranks until sync_owned()
   unsigned hs_blocks_ = 4096;  // grid cap of the cross Hessian-vector row pass
@@ -1547,7 +1605,8 @@ template <typename real> class Problem final : public ProblemBase {
   DevSide<real> U_, V_, T_;
   std::vector<Block> blocks_;
   std::vector<DevBuf<real>> W_, H_, P_, Q_;
-  DevBuf<real> acc_, G_, S_, Vd_, Rv_, Hv_, h_, M_, QTQ_, wpart_;
+  DevBuf<real> acc_, G_, S_, Vd_, Rv_, Hv_, h_, M_, wpart_;
+  const real *qtq_ = nullptr;  // this cross half's Q^T Q: a slot of M_
   DevBuf<unsigned> tick_;
   DevBuf<double> sums_, vecs_, part_, at_d_, popular_;
   DevBuf<uint8_t> cold_;
@@ -1684,6 +1743,24 @@ int ocffm_data_get_info(const ocffm_data *d, ocffm_data_info *o) {
 int ocffm_data_get_ds(const ocffm_data *d, uint64_t *out) {
   return guarded([&] {
     for (size_t i = 0; i < d->d.Ds.size(); i++) out[i] = d->d.Ds[i];
+  });
+}
+
+int ocffm_data_get_labels(const ocffm_data *d, uint64_t *yptr, uint64_t *ycol) {
+  return guarded([&] {
+    if (yptr) std::copy(d->d.yptr.begin(), d->d.yptr.end(), yptr);
+    if (ycol) std::copy(d->d.ycol.begin(), d->d.ycol.end(), ycol);
+  });
+}
+
+int ocffm_data_get_field(const ocffm_data *d, uint32_t field, int64_t *xptr, uint32_t *xidx, double *xval,
+                         uint64_t *nnz) {
+  return guarded([&] {
+    if (field >= d->d.f) throw ocffm::Error(OCFFM_E_ARG, "no such field");
+    if (nnz) *nnz = d->d.xidx[field].size();
+    if (xptr) std::copy(d->d.xptr[field].begin(), d->d.xptr[field].end(), xptr);
+    if (xidx) std::copy(d->d.xidx[field].begin(), d->d.xidx[field].end(), xidx);
+    if (xval) std::copy(d->d.xval[field].begin(), d->d.xval[field].end(), xval);
   });
 }
 

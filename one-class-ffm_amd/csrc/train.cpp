@@ -9,6 +9,7 @@
 //   --fp32 / --fp64 (default fp64, the reference's arithmetic type),
 //   --device N.
 #include <cctype>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -86,7 +87,14 @@ int main(int argc, char **argv) {
     if (i + 1 >= argc) throw std::invalid_argument("training data not specified");
     const std::string item_path = argv[i], tr_path = argv[i + 1];
 
-    // train.cpp:177-196
+    // train.cpp:177-196.  OCFFM_TIMING=1: phase wall times on stderr.
+    const bool timing = std::getenv("OCFFM_TIMING") != nullptr;
+    auto t_prev = std::chrono::steady_clock::now();
+    auto phase = [&](const char *name) {
+      const auto t = std::chrono::steady_clock::now();
+      if (timing) std::fprintf(stderr, "[timing] %-8s %9.3f ms\n", name, std::chrono::duration<double, std::milli>(t - t_prev).count());
+      t_prev = t;
+    };
     ocffm_data *U = nullptr, *V = nullptr, *Ut = nullptr;
     check(ocffm_data_read(tr_path.c_str(), 1, nullptr, 0, &U));
     check(ocffm_data_read(item_path.c_str(), 0, nullptr, 0, &V));
@@ -99,15 +107,21 @@ int main(int argc, char **argv) {
       check(ocffm_data_read(te_path.c_str(), 1, ds, (uint32_t)info.f, &Ut));
       delete[] ds;
     }
+    phase("read");
     ocffm_problem *prob = nullptr;
     check(ocffm_problem_create(U, Ut, V, &prm, &prob));
+    phase("create");
     // The reference's init is the first consumer of the process rand()
     // stream (implicit seed 1, ffm.cpp:72); HIP/RCCL start-up above may have
     // drawn from it, so restore that state before the draws.
     std::srand(1);
     check(ocffm_problem_init(prob));
+    check(ocffm_problem_sync(prob));
+    phase("init");
     check(ocffm_problem_solve(prob));
+    phase("solve");
     if (!model_path.empty()) check(ocffm_problem_save_model(prob, model_path.c_str()));
+    phase("save");
     ocffm_problem_destroy(prob);
     ocffm_data_free(U);
     ocffm_data_free(V);

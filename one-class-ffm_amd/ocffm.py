@@ -59,7 +59,7 @@ ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p)
 EXPORTS = [
     "ocffm_param_default", "ocffm_last_error", "ocffm_device_count", "ocffm_data_read",
     "ocffm_data_from_rows", "ocffm_data_trans_y", "ocffm_data_get_info", "ocffm_data_get_ds",
-    "ocffm_data_free", "ocffm_problem_create", "ocffm_comm_id", "ocffm_problem_create_dist",
+    "ocffm_data_get_labels", "ocffm_data_get_field", "ocffm_data_free", "ocffm_problem_create", "ocffm_comm_id", "ocffm_problem_create_dist",
     "ocffm_problem_create_dist_host", "ocffm_problem_init", "ocffm_problem_one_epoch",
     "ocffm_problem_solve_block", "ocffm_problem_cache_sasb", "ocffm_problem_solve",
     "ocffm_problem_validate", "ocffm_print_header", "ocffm_print_epoch", "ocffm_problem_get",
@@ -89,6 +89,8 @@ def lib():
     L.ocffm_data_trans_y.argtypes = [vp, vp]
     L.ocffm_data_get_info.argtypes = [vp, C.POINTER(_Info)]
     L.ocffm_data_get_ds.argtypes = [vp, vp]
+    L.ocffm_data_get_labels.argtypes = [vp, vp, vp]
+    L.ocffm_data_get_field.argtypes = [vp, u32, vp, vp, vp, vp]
     L.ocffm_data_free.argtypes = [vp]
     L.ocffm_data_free.restype = None
     L.ocffm_problem_create.argtypes = [vp, vp, vp, C.POINTER(_Param), C.POINTER(vp)]
@@ -202,6 +204,24 @@ class ImpData:
         out = np.zeros(max(1, self.info["f"]), dtype=np.uint64)
         _check(lib().ocffm_data_get_ds(self.h, _ptr(out)))
         return out[: self.info["f"]]
+
+    def labels(self):
+        """(yptr, ycol) as parsed (ffm.cpp:93-101)."""
+        i = self.info
+        yptr = np.zeros(i["m"] + 1, dtype=np.uint64)
+        ycol = np.zeros(max(1, i["nnz_y"]), dtype=np.uint64)
+        _check(lib().ocffm_data_get_labels(self.h, _ptr(yptr), _ptr(ycol)))
+        return yptr, ycol[: i["nnz_y"]]
+
+    def field(self, fi: int):
+        """(xptr, xidx, xval) of one field after split_fields (ffm.cpp:185-257)."""
+        nnz = C.c_uint64(0)
+        _check(lib().ocffm_data_get_field(self.h, fi, None, None, None, C.byref(nnz)))
+        xptr = np.zeros(self.info["m"] + 1, dtype=np.int64)
+        xidx = np.zeros(max(1, nnz.value), dtype=np.uint32)
+        xval = np.zeros(max(1, nnz.value), dtype=np.float64)
+        _check(lib().ocffm_data_get_field(self.h, fi, _ptr(xptr), _ptr(xidx), _ptr(xval), C.byref(nnz)))
+        return xptr, xidx[: nnz.value], xval[: nnz.value]
 
     def __del__(self):
         if getattr(self, "h", None) and _lib is not None:

@@ -131,3 +131,60 @@ def test_problem_needs_trans_y_and_valid_labels(tiny):
         ocffm.ImpProblem(U, None, V, ocffm.Parameter())
     # without a GPU the create call fails loudly with E_HIP before the check
     assert e.value.code in (ocffm.E_STATE, ocffm.E_HIP)
+
+
+def _read_all(path, has_label, chunks, monkeypatch, ds=None):
+    monkeypatch.setenv("OCFFM_PARSE_CHUNKS", str(chunks))
+    d = ocffm.ImpData.read(path, has_label, ds)
+    out = dict(info=d.info, Ds=d.Ds.copy())
+    if has_label:
+        out["labels"] = d.labels()
+    out["fields"] = [d.field(fi) for fi in range(d.info["f"])]
+    return out
+
+
+def _assert_same(a, b):
+    assert a["info"] == b["info"]
+    np.testing.assert_array_equal(a["Ds"], b["Ds"])
+    if "labels" in a:
+        for x, y in zip(a["labels"], b["labels"]):
+            np.testing.assert_array_equal(x, y)
+    for fa, fb in zip(a["fields"], b["fields"]):
+        for x, y in zip(fa, fb):
+            np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("chunks", [2, 3, 7, 16])
+def test_chunked_parser_equals_serial(tmp_path, monkeypatch, chunks):
+    """The parallel parser (line-aligned chunks joined in file order) gives the
+    serial read, including blank lines that re-use an earlier chunk's label
+    block (ffm.cpp:93) and lines cut short by an unparseable token."""
+    rng = np.random.default_rng(3)
+    lines = []
+    for i in range(600):
+        r = rng.random()
+        if r < 0.15:
+            lines.append("" if rng.random() < 0.5 else "  \t")
+            continue
+        labels = ",".join(str(x) for x in rng.integers(0, 40, size=rng.integers(1, 4)))
+        feats = [f"{rng.integers(0, 3)}:{rng.integers(0, 50)}:{rng.choice(['1', '0.5', '2.25e-1', '3'])}"
+                 for _ in range(rng.integers(0, 5))]
+        if r > 0.95:
+            feats.insert(1, "junk")
+        lines.append(labels + " " + " ".join(feats))
+    lines[:3] = ["", "", "1 0:1:1"]  # leading blank lines keep the initial (empty) block
+    text = "\n".join(lines) + "\n"
+    tr = _write(tmp_path, "tr", text)
+    ref = _read_all(tr, True, 1, monkeypatch)
+    _assert_same(_read_all(tr, True, chunks, monkeypatch), ref)
+    it = _write(tmp_path, "it", EDGE_ITEM * 50)
+    _assert_same(_read_all(it, False, chunks, monkeypatch), _read_all(it, False, 1, monkeypatch))
+    ds = np.array([10, 20, 30], dtype=np.uint64)
+    _assert_same(_read_all(tr, True, chunks, monkeypatch, ds), _read_all(tr, True, 1, monkeypatch, ds))
+    # a malformed label block fails the chunked read like the serial one
+    bad = _write(tmp_path, "bad", text + "1,,2 0:1:1\n" + text)
+    for c in (1, chunks):
+        monkeypatch.setenv("OCFFM_PARSE_CHUNKS", str(c))
+        with pytest.raises(ocffm.OcffmError) as e:
+            ocffm.ImpData.read(bad, True)
+        assert e.value.code == ocffm.E_ARG

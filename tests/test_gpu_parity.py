@@ -199,8 +199,8 @@ def test_heavy_columns(precision):
         assert abs(gpu_objective(o2, g) - f_ref) <= 1e-3 * abs(f_ref)
 
 
-@pytest.mark.parametrize("env", [{"OCFFM_FUSE": "1"}, {"OCFFM_SEG_LEN": "3"}, {"OCFFM_LOOKAHEAD": "3"},
-                                 {"OCFFM_FUSE": "1", "OCFFM_SEG_LEN": "2"}])
+@pytest.mark.parametrize("env", [{"OCFFM_FUSE": "2"}, {"OCFFM_FUSE": "0"}, {"OCFFM_SEG_LEN": "3"}, {"OCFFM_LOOKAHEAD": "3"},
+                                 {"OCFFM_FUSE": "2", "OCFFM_SEG_LEN": "2"}])
 def test_execution_variants_fp64(kk_small, monkeypatch, env):
     """Schedule knobs (id-field row fusion, segment length, CG look-ahead)
     change the kernels that run, never the result."""

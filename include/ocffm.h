@@ -205,6 +205,54 @@ int ocffm_problem_alg_bytes(ocffm_problem *p, double *bytes);
 int ocffm_problem_sync(ocffm_problem *p);
 void ocffm_problem_destroy(ocffm_problem *p);
 
+/* ------------------------------------------------------------ SGD mode
+ * BASELINE.json north_star extras, NO reference counterpart (the reference
+ * trains only by block Newton-CG): field-aware FM trained per instance by
+ * SGD / AdaGrad with lock-free (HOGWILD) writes to W, each positive
+ * (user row, item row) of U drawing `nneg` negatives on the device from an
+ * alias table over item popularity^neg_power; log-loss.  Instance nodes =
+ * the user row's nodes then the item row's (global feature id = field
+ * offset + idx).  Parity against oracle/sgd_oracle.cpp (a serial CPU
+ * statement), not against the reference ("parity unpinned"). */
+typedef struct ocffm_sgd ocffm_sgd;
+typedef struct ocffm_sgd_param {
+  uint32_t k;          /* latent dimension (1..128)                         */
+  float eta;           /* learning rate (libffm default 0.2)                */
+  float lambda;        /* L2 (libffm default 2e-5)                          */
+  uint32_t nneg;       /* sampled negatives per positive                    */
+  double neg_power;    /* alias weights = item label count ^ neg_power      */
+  int32_t adagrad;     /* 1: AdaGrad (G starts at 1), 0: plain SGD          */
+  int32_t norm;        /* 1: instance-wise 1/|x|^2 normalisation            */
+  int32_t serial;      /* 1: one wave, instances in order (parity tests)    */
+  uint64_t seed;       /* W init, instance order, negative draws            */
+  int32_t device;
+} ocffm_sgd_param;
+typedef struct ocffm_sgd_info {
+  uint64_t n_features; /* NF: rows of W (all fields)      */
+  uint32_t n_fields;   /* F                               */
+  uint32_t kp;         /* padded row length               */
+  uint64_t positives;  /* this rank's positives           */
+  uint64_t instances;  /* per epoch: positives (1 + nneg) */
+} ocffm_sgd_info;
+void ocffm_sgd_param_default(ocffm_sgd_param *p);
+int ocffm_sgd_create(const ocffm_data *U, const ocffm_data *V, const ocffm_sgd_param *p, ocffm_sgd **out);
+/* One process per GPU: this rank trains on its contiguous user shard's
+ * positives; ocffm_sgd_average() makes W and G the mean over the ranks
+ * (RCCL all-reduce over xGMI) — periodic model averaging. */
+int ocffm_sgd_create_dist(const ocffm_data *U, const ocffm_data *V, const ocffm_sgd_param *p, int rank, int nranks,
+                          const void *comm_id, ocffm_sgd **out);
+int ocffm_sgd_epoch(ocffm_sgd *s, double *mean_loss);
+int ocffm_sgd_average(ocffm_sgd *s);
+/* phi for n (user row, item row) pairs with the current W. */
+int ocffm_sgd_phi(ocffm_sgd *s, uint64_t n, const uint32_t *users, const uint32_t *items, float *out);
+/* what: 'W' / 'G' (float, NF x F x kp), 'p' alias probabilities (float),
+ * 'a' alias targets (uint32), 'o' last epoch's order (uint64 A, B, T). */
+int ocffm_sgd_get(ocffm_sgd *s, char what, void *out, uint64_t cap, uint64_t *len);
+int ocffm_sgd_set_w(ocffm_sgd *s, const float *w, uint64_t n);
+int ocffm_sgd_get_info(ocffm_sgd *s, ocffm_sgd_info *out);
+int ocffm_sgd_sync(ocffm_sgd *s);
+void ocffm_sgd_destroy(ocffm_sgd *s);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1391,7 +1391,7 @@ __global__ __launch_bounds__(BLOCK) void k_scores(uint64_t rows, uint64_t row0, 
 // z[argmax] = MIN_Z (-1000) and first-index tie-break, accumulating hits and
 // DCG/IDCG at the cut-offs 5,10,20,40,80 (validate/prec_k/ndcg,
 // ffm.cpp:982-1128).  One block per row.  out[r] = {ploss, hits[5], ndcg[5]}.
-__global__ __launch_bounds__(BLOCK) void k_rank(uint64_t rows, uint64_t row0, uint64_t n, uint64_t max_z,
+static __global__ __launch_bounds__(BLOCK) void k_rank(uint64_t rows, uint64_t row0, uint64_t n, uint64_t max_z,
                                                 double *__restrict__ z, const int64_t *__restrict__ lptr,
                                                 const uint32_t *__restrict__ lcol, const uint8_t *__restrict__ cold,
                                                 uint64_t npop, const double *__restrict__ at,

@@ -68,6 +68,9 @@ EXPORTS = [
     "ocffm_problem_kernel_stats",
     "ocffm_problem_reset_stats", "ocffm_problem_alg_bytes", "ocffm_problem_sync",
     "ocffm_problem_destroy",
+    "ocffm_sgd_param_default", "ocffm_sgd_create", "ocffm_sgd_create_dist", "ocffm_sgd_epoch",
+    "ocffm_sgd_average", "ocffm_sgd_phi", "ocffm_sgd_get", "ocffm_sgd_set_w", "ocffm_sgd_get_info",
+    "ocffm_sgd_sync", "ocffm_sgd_destroy",
 ]
 
 _lib = None
@@ -116,6 +119,19 @@ def lib():
     L.ocffm_problem_alg_bytes.argtypes = [vp, C.POINTER(dbl)]
     L.ocffm_problem_destroy.argtypes = [vp]
     L.ocffm_problem_destroy.restype = None
+    L.ocffm_sgd_param_default.argtypes = [vp]
+    L.ocffm_sgd_param_default.restype = None
+    L.ocffm_sgd_create.argtypes = [vp, vp, vp, C.POINTER(vp)]
+    L.ocffm_sgd_create_dist.argtypes = [vp, vp, vp, i32, i32, vp, C.POINTER(vp)]
+    L.ocffm_sgd_epoch.argtypes = [vp, C.POINTER(dbl)]
+    L.ocffm_sgd_average.argtypes = [vp]
+    L.ocffm_sgd_phi.argtypes = [vp, u64, vp, vp, vp]
+    L.ocffm_sgd_get.argtypes = [vp, C.c_char, vp, u64, C.POINTER(u64)]
+    L.ocffm_sgd_set_w.argtypes = [vp, vp, u64]
+    L.ocffm_sgd_get_info.argtypes = [vp, vp]
+    L.ocffm_sgd_sync.argtypes = [vp]
+    L.ocffm_sgd_destroy.argtypes = [vp]
+    L.ocffm_sgd_destroy.restype = None
     _lib = L
     return L
 
@@ -227,6 +243,85 @@ class ImpData:
         if getattr(self, "h", None) and _lib is not None:
             _lib.ocffm_data_free(self.h)
             self.h = None
+
+
+class _SgdParam(C.Structure):
+    _fields_ = [("k", C.c_uint32), ("eta", C.c_float), ("lambda_", C.c_float), ("nneg", C.c_uint32),
+                ("neg_power", C.c_double), ("adagrad", C.c_int32), ("norm", C.c_int32), ("serial", C.c_int32),
+                ("seed", C.c_uint64), ("device", C.c_int32)]
+
+
+class _SgdInfo(C.Structure):
+    _fields_ = [("n_features", C.c_uint64), ("n_fields", C.c_uint32), ("kp", C.c_uint32),
+                ("positives", C.c_uint64), ("instances", C.c_uint64)]
+
+
+class SgdTrainer:
+    """Field-aware FM by per-instance SGD / AdaGrad with HOGWILD writes and
+    on-device negative sampling (include/ocffm.h, SGD mode).  North-star
+    extra with no reference counterpart: parity is against
+    oracle/sgd_oracle.cpp, not the reference."""
+
+    def __init__(self, U: "ImpData", V: "ImpData", rank: int = 0, nranks: int = 1, comm: Optional[bytes] = None,
+                 **kw):
+        p = _SgdParam()
+        lib().ocffm_sgd_param_default(C.byref(p))
+        for key, val in kw.items():
+            setattr(p, "lambda_" if key == "lambda" else key, val)
+        self.param = p
+        self._keep = (U, V)
+        h = C.c_void_p()
+        if nranks > 1 or comm is not None:
+            idb = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(comm)
+            _check(lib().ocffm_sgd_create_dist(U.h, V.h, C.byref(p), rank, nranks, idb, C.byref(h)))
+        else:
+            _check(lib().ocffm_sgd_create(U.h, V.h, C.byref(p), C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.ocffm_sgd_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    @property
+    def info(self) -> dict:
+        i = _SgdInfo()
+        _check(lib().ocffm_sgd_get_info(self.h, C.byref(i)))
+        return dict(n_features=i.n_features, n_fields=i.n_fields, kp=i.kp, positives=i.positives,
+                    instances=i.instances)
+
+    def epoch(self) -> float:
+        loss = C.c_double(0)
+        _check(lib().ocffm_sgd_epoch(self.h, C.byref(loss)))
+        return loss.value
+
+    def average(self) -> None:
+        _check(lib().ocffm_sgd_average(self.h))
+
+    def phi(self, users, items) -> np.ndarray:
+        u = np.ascontiguousarray(users, dtype=np.uint32)
+        v = np.ascontiguousarray(items, dtype=np.uint32)
+        out = np.zeros(max(1, u.size), dtype=np.float32)
+        _check(lib().ocffm_sgd_phi(self.h, u.size, _ptr(u), _ptr(v), _ptr(out)))
+        return out[: u.size]
+
+    def get(self, what: str) -> np.ndarray:
+        n = C.c_uint64(0)
+        _check(lib().ocffm_sgd_get(self.h, what.encode(), None, 0, C.byref(n)))
+        dt = {"W": np.float32, "G": np.float32, "p": np.float32, "a": np.uint32, "o": np.uint64}[what]
+        out = np.zeros(max(1, n.value), dtype=dt)
+        _check(lib().ocffm_sgd_get(self.h, what.encode(), _ptr(out), n.value, C.byref(n)))
+        return out[: n.value]
+
+    def set_w(self, w) -> None:
+        a = np.ascontiguousarray(w, dtype=np.float32)
+        _check(lib().ocffm_sgd_set_w(self.h, _ptr(a), a.size))
+
+    def sync(self) -> None:
+        _check(lib().ocffm_sgd_sync(self.h))
 
 
 def comm_id() -> bytes:

@@ -25,6 +25,7 @@
 #include <memory>
 #include <type_traits>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -39,7 +40,8 @@ namespace ocffm {
 namespace sgd {
 
 constexpr int NMAX = 64;  // nodes per instance: one per lane
-constexpr int SPG = 8;    // slots per subgroup held in registers (slots <= SPG * NSG)
+constexpr int SPG_MAX = 8;  // slots per subgroup held in registers (slots <= SPG * NSG); the
+                            // launch picks the smallest of 2, 4, 8 that covers the widest instance
 
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -71,52 +73,113 @@ __device__ __forceinline__ uint32_t draw_item(const Args &d, uint64_t qq, uint64
   }
   y = -1.0f;
   const uint64_t h = mix64(d.seed + 0x9E3779B97F4A7C15ULL * (d.epoch * d.T + qq));
-  const uint64_t idx = (h >> 32) % d.n_items;
+  const uint32_t idx = (uint32_t)(h >> 32) % (uint32_t)d.n_items;  // n_items < 2^32
   const float coin = (float)(uint32_t)(h & 0xffffffu) * (1.0f / 16777216.0f);
   return coin < d.prob[idx] ? (uint32_t)idx : d.alias[idx];
 }
 
-// One wave per instance (grid-stride): nodes in lanes 0..n-1; forward pass
-// over the n(n-1)/2 pairs spread over the NSG subgroups (a pair's two rows
-// are 16-B-per-lane loads, its dot a DPP subgroup sum); then every slot
-// (a, f) with a partner in field f computes its step from the pre-step rows
-// into registers, and the writes follow (plain stores: HOGWILD).
-template <int KP>
-__global__ __launch_bounds__(256) void k_sgd(Args d) {
+// Nodes of one instance, lane l < n holding node l (user row, then item row).
+struct Nodes {
+  uint32_t j, f;
+  float x;
+  int n;
+};
+__device__ __forceinline__ Nodes load_nodes(const Args &d, uint32_t u, uint32_t it, int lane) {
+  const uint64_t ub = d.uptr[u], vb = d.vptr[it];
+  const int nu = (int)(d.uptr[u + 1] - ub);
+  Nodes o{0u, 0xffffffffu, 0.0f, nu + (int)(d.vptr[it + 1] - vb)};
+  if (lane < nu) {
+    o.j = d.unode[ub + lane];
+    o.f = d.ufld[ub + lane];
+    o.x = d.uval[ub + lane];
+  } else if (lane < o.n) {
+    o.j = d.vnode[vb + lane - nu];
+    o.f = d.vfld[vb + lane - nu];
+    o.x = d.vval[vb + lane - nu];
+  }
+  return o;
+}
+
+// One wave per instance (grid-stride).  Slot (a, f) = row w[j_a][f] of node
+// a for field f; it takes part iff another node b != a sits in field f.  The
+// wave's subgroups load their slots' W rows (and AdaGrad rows) in one round
+// into registers and stage the W rows in this wave's LDS region; the
+// forward pass (pair (a, b) = <slot(a, f_b), slot(b, f_a)>) and every slot's
+// gradient sum_{b != a, f_b = f} x_b slot(b, f_a) then read LDS only, and the
+// steps are stored (plain stores: HOGWILD).  LDS per wave: SMAX rows.
+template <int KP, int SPG, int OCC>
+__global__ __launch_bounds__(256, OCC) void k_sgd(Args d, int smax) {
   using Gm = Geo<float, KP>;
   constexpr int LPR = Gm::LPR, NG = Gm::NSG;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
   const int lane = threadIdx.x & 63, g = lane / LPR, li = lane % LPR;
+  float *sl = reinterpret_cast<float *>(smem_raw) + (size_t)(threadIdx.x >> 6) * smax * KP;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   const uint32_t F = d.F;
   double lsum = 0;
+  // qq = (A q + B) mod T stepped incrementally over this wave's q (one
+  // 64-bit modulo per wave, not per instance)
+  const uint64_t step = (d.A * (nwaves % d.T)) % d.T;
+  uint64_t qq = (d.A * (wave % d.T) + d.B) % d.T;
+  const uint32_t m1 = 1 + d.nneg;
   for (uint64_t q = wave; q < d.T; q += nwaves) {
-    const uint64_t qq = (d.A * q + d.B) % d.T;
-    const uint64_t p = qq / (1 + d.nneg), r = qq % (1 + d.nneg);
-    const uint32_t u = d.pu[p];
+    uint64_t p, r;
+    if (d.T < (1ull << 32)) {
+      const uint32_t q32 = (uint32_t)qq, p32 = q32 / m1;
+      p = p32;
+      r = q32 - p32 * m1;
+    } else {
+      p = qq / m1;
+      r = qq - p * m1;
+    }
     float y;
     const uint32_t it = draw_item(d, qq, p, r, y);
-    const uint64_t ub = d.uptr[u], vb = d.vptr[it];
-    const int nu = (int)(d.uptr[u + 1] - ub), n = nu + (int)(d.vptr[it + 1] - vb);
-    uint32_t nj = 0, nf = 0xffffffffu;
-    float nx = 0;
-    if (lane < nu) {
-      nj = d.unode[ub + lane];
-      nf = d.ufld[ub + lane];
-      nx = d.uval[ub + lane];
-    } else if (lane < n) {
-      nj = d.vnode[vb + lane - nu];
-      nf = d.vfld[vb + lane - nu];
-      nx = d.vval[vb + lane - nu];
-    }
+    qq += step;
+    if (qq >= d.T) qq -= d.T;
+    const Nodes nd = load_nodes(d, d.pu[p], it, lane);
+    const int n = nd.n, S = n * (int)F;
+    // field populations (F <= 64): count of nodes per field, per lane f
+    int fcnt = 0;
+    for (int b = 0; b < n; b++) fcnt += (__builtin_amdgcn_readlane((int)nd.f, b) == lane) ? 1 : 0;
     float rn = 1.0f;
     if (d.norm) {
-      float s = nx * nx;
+      float s2 = nd.x * nd.x;
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-      rn = s > 0 ? 1.0f / s : 1.0f;
+      for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
+      rn = s2 > 0 ? 1.0f / s2 : 1.0f;
     }
-    // forward
+    // slot rows: one round of loads, W staged in LDS
+    // (lane moves of node data happen here, with every lane active: a
+    // ds_bpermute from a lane outside EXEC does not return its value)
+    f4v gr[SPG];
+    bool act[SPG];
+    uint32_t sja[SPG], sfa[SPG];
+    float sxa[SPG];
+    {
+      f4v wr[SPG];
+#pragma unroll
+      for (int t = 0; t < SPG; t++) {
+        const int s = g + t * NG;
+        const int a = min(s / (int)F, 63);
+        const int fl = s % (int)F;
+        sja[t] = __shfl(nd.j, a, 64);
+        sfa[t] = __shfl(nd.f, a, 64);
+        sxa[t] = __shfl(nd.x, a, 64);
+        const int c = __shfl(fcnt, fl, 64) - (sfa[t] == (uint32_t)fl ? 1 : 0);
+        act[t] = s < S && c > 0;
+        if (act[t]) wr[t] = vld<float>(d.W + ((size_t)sja[t] * F + fl) * KP + li * 4);
+      }
+#pragma unroll
+      for (int t = 0; t < SPG; t++)
+        if (act[t]) {
+          vst<float>(sl + (size_t)(g + t * NG) * KP + li * 4, wr[t]);
+          if (d.adagrad) gr[t] = vld<float>(d.G + ((size_t)sja[t] * F + (g + t * NG) % (int)F) * KP + li * 4);
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // forward over the pairs, from LDS
     const int npairs = n * (n - 1) / 2;
     float acc = 0;
     for (int base = 0; base < npairs; base += NG) {
@@ -127,11 +190,11 @@ __global__ __launch_bounds__(256) void k_sgd(Args d) {
         a++;
       }
       const int b = a + 1 + rem;
-      const uint32_t ja = __shfl(nj, a, 64), fa = __shfl(nf, a, 64), jb = __shfl(nj, b, 64), fb = __shfl(nf, b, 64);
-      const float xab = __shfl(nx, a, 64) * __shfl(nx, b, 64);
+      const uint32_t fa = __shfl(nd.f, a, 64), fb = __shfl(nd.f, b, 64);
+      const float xab = __shfl(nd.x, a, 64) * __shfl(nd.x, b, 64);
       if (base + g < npairs) {
-        const f4v wa = vld<float>(d.W + ((size_t)ja * F + fb) * KP + li * 4);
-        const f4v wb = vld<float>(d.W + ((size_t)jb * F + fa) * KP + li * 4);
+        const f4v wa = vld<float>(sl + ((size_t)a * F + fb) * KP + li * 4);
+        const f4v wb = vld<float>(sl + ((size_t)b * F + fa) * KP + li * 4);
         acc += sg_sum<LPR>(hsum<float>(wa * wb)) * xab;
       }
     }
@@ -139,53 +202,36 @@ __global__ __launch_bounds__(256) void k_sgd(Args d) {
     const float ex = expf(-y * phi);
     const float kappa = -y * ex / (1.0f + ex);
     if (lane == 0) lsum += log1p((double)ex);
-    // slot steps from the pre-step rows
-    const int S = n * (int)F;
-    f4v wn[SPG], gn[SPG];
-    size_t off[SPG];
-    bool ok[SPG];
+    // slot steps
 #pragma unroll
     for (int t = 0; t < SPG; t++) {
+      if (!act[t]) continue;
       const int s = g + t * NG;
-      ok[t] = false;
-      off[t] = 0;
-      const int a = min(s / (int)F, 63);
+      const int a = s / (int)F;
       const uint32_t fl = (uint32_t)(s % (int)F);
-      const uint32_t ja = __shfl(nj, a, 64), fa = __shfl(nf, a, 64);
-      const float xa = __shfl(nx, a, 64);
+      const uint32_t ja = sja[t], fa = sfa[t];
+      const float xa = sxa[t];
       f4v sacc = vzero<float>();
-      bool any = false;
-      for (int b = 0; b < n; b++) {  // wave-uniform
-        const uint32_t jb = (uint32_t)__builtin_amdgcn_readlane((int)nj, b);
-        const uint32_t fb = (uint32_t)__builtin_amdgcn_readlane((int)nf, b);
-        const float xb = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, nx), b));
-        if (s < S && b != a && fb == fl) {
-          sacc += vsplat<float>(xb) * vld<float>(d.W + ((size_t)jb * F + fa) * KP + li * 4);
-          any = true;
-        }
+      for (int b = 0; b < n; b++) {  // wave-uniform trip count
+        const uint32_t fb = (uint32_t)__builtin_amdgcn_readlane((int)nd.f, b);
+        const float xb = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, nd.x), b));
+        if (b != a && fb == fl) sacc += vsplat<float>(xb) * vld<float>(sl + ((size_t)b * F + fa) * KP + li * 4);
       }
-      if (s < S && any) {
-        off[t] = ((size_t)ja * F + fl) * KP + li * 4;
-        const f4v w = vld<float>(d.W + off[t]);
-        const f4v gr = vsplat<float>(d.lam) * w + vsplat<float>(kappa * rn * xa) * sacc;
-        if (d.adagrad) {
-          gn[t] = vld<float>(d.G + off[t]) + gr * gr;
-          f4v st;
+      const size_t off = ((size_t)ja * F + fl) * KP + li * 4;
+      const f4v w = vld<float>(sl + (size_t)s * KP + li * 4);
+      const f4v gd = vsplat<float>(d.lam) * w + vsplat<float>(kappa * rn * xa) * sacc;
+      if (d.adagrad) {
+        const f4v gv = gr[t] + gd * gd;
+        f4v st;
 #pragma unroll
-          for (int e = 0; e < 4; e++) st[e] = d.eta * gr[e] / sqrtf(gn[t][e]);
-          wn[t] = w - st;
-        } else {
-          wn[t] = w - vsplat<float>(d.eta) * gr;
-        }
-        ok[t] = true;
+        for (int e = 0; e < 4; e++) st[e] = d.eta * gd[e] * __builtin_amdgcn_rsqf(gv[e]);  // 1-ulp rsq
+        vst<float>(d.W + off, w - st);
+        vst<float>(d.G + off, gv);
+      } else {
+        vst<float>(d.W + off, w - vsplat<float>(d.eta) * gd);
       }
     }
-#pragma unroll
-    for (int t = 0; t < SPG; t++)
-      if (ok[t]) {
-        vst<float>(d.W + off[t], wn[t]);
-        if (d.adagrad) vst<float>(d.G + off[t], gn[t]);
-      }
+    __builtin_amdgcn_wave_barrier();  // LDS reads of this instance before the next one's writes
   }
   if (lane == 0 && lsum != 0) atomicAdd(d.loss, lsum);
 }
@@ -285,9 +331,13 @@ class Trainer {
     build_nodes(V, fu_, off, vptr_, vnode_, vfld_, vval_, vmax);
     const int nmax = umax + vmax;
     const int ng = 64 / std::max<int>(1, (int)(kp_ / 4));
-    if (nmax > NMAX || (uint64_t)nmax * F_ > (uint64_t)SPG * ng)
+    smax_ = std::max(1, nmax * (int)F_);
+    if (F_ > 64) throw Error(OCFFM_E_ARG, "more than 64 fields in the SGD mode");
+    if (nmax > NMAX || (uint64_t)nmax * F_ > (uint64_t)SPG_MAX * ng)
       throw Error(OCFFM_E_ARG, "instances too wide for the SGD kernel (nodes " + std::to_string(nmax) + " x fields " +
-                                   std::to_string(F_) + " > " + std::to_string(SPG * ng) + " slots at this k)");
+                                   std::to_string(F_) + " > " + std::to_string(SPG_MAX * ng) + " slots at this k)");
+    spg_ = 2;
+    while ((uint64_t)nmax * F_ > (uint64_t)spg_ * ng) spg_ *= 2;
     // positives of this rank's user shard
     for (uint64_t j : U.ycol)
       if (j >= V.m) throw Error(OCFFM_E_DATA, "train label >= number of item rows");
@@ -365,7 +415,21 @@ class Trainer {
         block = 256;
         grid = (unsigned)std::min<uint64_t>((T_ + 3) / 4, 2048);
       }
-      launch_kp([&](auto K) { hipLaunchKernelGGL(k_sgd<decltype(K)::value>, grid, block, 0, stream_, a); });
+      const int smax = smax_;
+      launch_kp([&](auto K) {
+        constexpr int KPc = decltype(K)::value;
+        const size_t smem = (size_t)(block / 64) * smax * KPc * sizeof(float);
+        // occupancy bound: 4 waves/SIMD (a few VGPRs spill) or the compiler's choice (3 at k=32)
+        if (occ4_) {
+          if (spg_ == 2) hipLaunchKernelGGL((k_sgd<KPc, 2, 4>), grid, block, smem, stream_, a, smax);
+          else if (spg_ == 4) hipLaunchKernelGGL((k_sgd<KPc, 4, 4>), grid, block, smem, stream_, a, smax);
+          else hipLaunchKernelGGL((k_sgd<KPc, 8, 4>), grid, block, smem, stream_, a, smax);
+        } else {
+          if (spg_ == 2) hipLaunchKernelGGL((k_sgd<KPc, 2, 1>), grid, block, smem, stream_, a, smax);
+          else if (spg_ == 4) hipLaunchKernelGGL((k_sgd<KPc, 4, 1>), grid, block, smem, stream_, a, smax);
+          else hipLaunchKernelGGL((k_sgd<KPc, 8, 1>), grid, block, smem, stream_, a, smax);
+        }
+      });
       HIPCHK(hipGetLastError());
     }
     double loss = 0;
@@ -539,6 +603,9 @@ class Trainer {
   hipStream_t stream_ = nullptr;
   ncclComm_t nccl_ = nullptr;
   uint32_t kp_ = 4, fu_ = 0, fv_ = 0, F_ = 0;
+  int smax_ = 1;  // slot rows per wave in LDS: max nodes x fields
+  int spg_ = 2;   // slots per subgroup of the k_sgd instantiation
+  bool occ4_ = std::getenv("OCFFM_SGD_OCC") == nullptr || std::atoi(std::getenv("OCFFM_SGD_OCC")) != 0;
   uint64_t nf_ = 0, P_ = 0, T_ = 0, n_items_ = 0, epoch_ = 0, last_A_ = 1, last_B_ = 0;
   uint64_t h_uptr_size_ = 0, h_vptr_size_ = 0;
   DevBuf<uint64_t> uptr_, vptr_;

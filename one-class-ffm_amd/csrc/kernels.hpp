@@ -1312,6 +1312,19 @@ __global__ __launch_bounds__(BLOCK) void k_reduce_parts(uint64_t nb, uint64_t no
   }
 }
 
+// out = sum_i v[i] in double (b_sum of gd_side, ffm.cpp:551): block sums,
+// then the last block combines them in block order (deterministic).
+template <typename real>
+__global__ __launch_bounds__(BLOCK) void k_vec_sum(uint64_t n, const real *__restrict__ v, double *__restrict__ out,
+                                                   double *part, unsigned *tick) {
+  double s = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK)
+    s += (double)v[i];
+  const double bv[1] = {block_sum(s)};
+  double tot[1];
+  if (last_block<1>(bv, part, tick, tot) && threadIdx.x == 0) out[0] = tot[0];
+}
+
 // Column sums of C tables at once (cache_sasb, ffm.cpp:514-535):
 // part[block][c*KP + d] = sum over the block's rows j of T_c[j][d].  Rows are
 // read 16 B per lane, BLOCK/LPR rows per pass; row groups are combined in

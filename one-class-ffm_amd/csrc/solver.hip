@@ -1195,7 +1195,7 @@ template <typename real> class Problem final : public ProblemBase {
   // gd_side / gd_cross (ffm.cpp:537-703) -> G, and the CG start vectors.
   void gradient(HalfCtx &h) {
     DevSide<real> &own = *h.own;
-    const bool fz_ = fused_rows(h);
+    const bool fz_ = fused_rows(h, false);
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
       using Gm = Geo<real, KP>;
@@ -1231,7 +1231,10 @@ template <typename real> class Problem final : public ProblemBase {
         qtq_ = M_.p + (size_t)c0 * KP * KP;
       } else {
         DevSide<real> &other = h.user ? V_ : U_;  // sum of the other side's bias (b_sum, ffm.cpp:551)
-        aggregates(other.R, 0, nullptr, nullptr, other.bias.p, nullptr);
+        prof_launch("bias_sum", (double)other.R * rs, [&] {
+          launch(k_vec_sum<real>, grid_for(other.R, BLOCK, 256), BLOCK, 0, (uint64_t)other.R,
+                 (const real *)other.bias.p, sums_.p + 2 * KP, part_.p, tick_.p);
+        });
         const double n1 = (double)other.R;
         const double bytes = (double)own.R * 8 + (double)own.npos * rs + (double)own.R * KP * rs * 2 +
                              (double)own.R * rs * 2;
@@ -1285,11 +1288,12 @@ template <typename real> class Problem final : public ProblemBase {
     return f;
   }
   // id-like field on one GPU: the row pass finalises its feature column.
-  // fuse_ 1: side halves only (a row is one feature, no partial sums); 2: cross
-  // halves too (multi-segment rows meet through column atomics: slower on
-  // Pareto-headed items).
-  bool fused_rows(const HalfCtx &h) const {
-    return h.F->idlike && !comm_.active() && (fuse_ >= 2 || (fuse_ == 1 && !h.cross));
+  // fuse_ 1: the Hessian-vector pass of side halves only (one row = one
+  // feature, no partial sums); 2: every row pass (the gradient passes and the
+  // cross halves walk positive segments, whose multi-segment rows meet through
+  // column atomics: slower on Pareto-headed items).
+  bool fused_rows(const HalfCtx &h, bool hv) const {
+    return h.F->idlike && !comm_.active() && (fuse_ >= 2 || (fuse_ == 1 && hv && !h.cross));
   }
 
   void scatter(HalfCtx &h, int it, bool seg) {
@@ -1366,7 +1370,7 @@ template <typename real> class Problem final : public ProblemBase {
   void hv_pass(HalfCtx &h, int it) {
     DevSide<real> &own = *h.own;
     const int *run = &st_.p->run[it];
-    const bool fz_ = fused_rows(h);
+    const bool fz_ = fused_rows(h, true);
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
       using Gm = Geo<real, KP>;

@@ -92,8 +92,16 @@ struct CgState {
 template <typename real> __device__ __forceinline__ vec_t<real> vld(const real *p) {
   return *reinterpret_cast<const vec_t<real> *>(p);
 }
+// Stores of pass outputs.  OCFFM_NT_STORES=1 at build time makes them
+// non-temporal (global_store ... nt): the bytes stream out instead of
+// sitting dirty in the XCD's L2 until the kernel-end write-back, which the
+// next (dependent) dispatch waits for.
+#ifndef OCFFM_NT_STORES
+#define OCFFM_NT_STORES 0
+#endif
 template <typename real> __device__ __forceinline__ void vst(real *p, vec_t<real> v) {
-  *reinterpret_cast<vec_t<real> *>(p) = v;
+  if constexpr (OCFFM_NT_STORES) __builtin_nontemporal_store(v, reinterpret_cast<vec_t<real> *>(p));
+  else *reinterpret_cast<vec_t<real> *>(p) = v;
 }
 template <typename real> __device__ __forceinline__ vec_t<real> vzero() {
   vec_t<real> v;

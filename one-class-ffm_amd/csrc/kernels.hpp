@@ -1288,6 +1288,91 @@ __global__ __launch_bounds__(BLOCK) void k_gram_part(uint64_t Rp, int L, const r
   }
 }
 
+// The same per-block partials as k_gram_part for fp32 rows of KP = 32, on
+// MFMA (v_mfma_f32_32x32x2f32): the Gram gram[l][e][d] = sum_j A_l[j][e] B[j][d]
+// is a 32 x 32 x (rows) product with the rows as the K dimension.  Operand
+// layouts: A lane l = A_l[j + l/32][l%32] (m = e), B lane l = B[j + l/32][l%32]
+// (n = d): each lane loads one dword per table per row pair, so a wave reads
+// two whole 128-B rows per load instruction, straight into the MFMA operand
+// registers (no LDS staging).  D register r of lane l is element
+// m = 8(r/4) + 4(l/32) + r%4, n = l%32.  The four waves of a block take
+// interleaved row pairs and are combined in wave order through LDS
+// (deterministic).  Column sums ride along on the B operand.
+template <int LMAX>
+__global__ __launch_bounds__(BLOCK) void k_gram_mfma32(uint64_t Rp, int L, const float *const *__restrict__ A,
+                                                      const float *__restrict__ B, const float *__restrict__ wv,
+                                                      double *__restrict__ part, uint64_t rows_per_block) {
+  typedef float f16x __attribute__((ext_vector_type(16)));
+  constexpr int U = 4;  // row pairs per wave per round
+  __shared__ float red[LMAX][1024];
+  __shared__ float redc[3][32];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int e = lane & 31, hf = lane >> 5;
+  f16x acc[LMAX];
+#pragma unroll
+  for (int c = 0; c < LMAX; c++)
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[c][r] = 0.0f;
+  const float *Ap[LMAX];
+#pragma unroll
+  for (int c = 0; c < LMAX; c++) Ap[c] = c < L ? A[c] : nullptr;
+  float cs = 0, ws = 0, wt = 0;
+  const uint64_t r0 = (uint64_t)blockIdx.x * rows_per_block;
+  const uint64_t r1 = min(Rp, r0 + rows_per_block);
+  for (uint64_t j0 = r0 + 2 * w; j0 < r1; j0 += 8 * U) {
+    float bv[U], wvv[U], av[U][LMAX];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t jj = j0 + 8 * u + hf;
+      const bool ok = jj < r1;
+      bv[u] = (ok && B) ? B[jj * 32 + e] : 0.0f;
+      wvv[u] = (ok && wv) ? wv[jj] : 0.0f;
+#pragma unroll
+      for (int c = 0; c < LMAX; c++) av[u][c] = (ok && c < L) ? Ap[c][jj * 32 + e] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+#pragma unroll
+      for (int c = 0; c < LMAX; c++)
+        if (c < L) acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u][c], bv[u], acc[c], 0, 0, 0);
+      cs += bv[u];
+      ws += wvv[u] * bv[u];
+      if (e == 0) wt += wvv[u];
+    }
+  }
+  // column sums: the two half-waves hold even / odd rows of the same column
+  cs += __shfl_xor(cs, 32, 64);
+  ws += __shfl_xor(ws, 32, 64);
+  wt += __shfl_xor(wt, 32, 64);
+  for (int ww = 0; ww < BLOCK / 64; ww++) {
+    if (w == ww) {
+#pragma unroll
+      for (int c = 0; c < LMAX; c++)
+        if (c < L)
+#pragma unroll
+          for (int r = 0; r < 16; r++) {
+            const int m = 8 * (r >> 2) + 4 * hf + (r & 3);
+            float &x = red[c][m * 32 + e];
+            x = (ww == 0 ? 0.0f : x) + acc[c][r];
+          }
+      if (hf == 0) {
+        redc[0][e] = (ww == 0 ? 0.0f : redc[0][e]) + cs;
+        redc[1][e] = (ww == 0 ? 0.0f : redc[1][e]) + ws;
+        if (e == 0) redc[2][0] = (ww == 0 ? 0.0f : redc[2][0]) + wt;
+      }
+    }
+    __syncthreads();
+  }
+  const size_t NOUT = (size_t)L * 1024 + 2 * 32 + 1;
+  double *out = part + (size_t)blockIdx.x * NOUT;
+  for (int o = threadIdx.x; o < L * 1024; o += BLOCK) out[o] = (double)red[o >> 10][o & 1023];
+  if (threadIdx.x < 32) {
+    out[(size_t)L * 1024 + threadIdx.x] = (double)redc[0][threadIdx.x];
+    out[(size_t)L * 1024 + 32 + threadIdx.x] = (double)redc[1][threadIdx.x];
+  }
+  if (threadIdx.x == 0) out[(size_t)L * 1024 + 64] = (double)redc[2][0];
+}
+
 // o in [0, cnt): t = sum_b part[b][off + o]; o < split -> out_real[o] = t,
 // else out_dbl[o - split] = t.  A block owns 16 consecutive outputs
 // (coalesced 128-B reads) and 16 groups of partial rows; groups are combined

@@ -1036,11 +1036,15 @@ template <typename real> class Problem final : public ProblemBase {
   // k_gram_part): M (L x KP x KP, real) = A_l^T B for the device pointer
   // list A, and sums_ = [sum B | sum wv*B | sum wv] (doubles).  A or B or wv
   // may be absent (L = 0, B = null, wv = null).
+  static constexpr int GRAM_LMAX = 8;  // tables per k_gram_mfma32 launch
+  bool mfma_gram(int L) const { return std::is_same<real, float>::value && kp_ == 32 && L >= 1 && !no_mfma_; }
+
   void aggregates(uint64_t Rp, int L, const real *const *A, const real *B, const real *wv, real *M) {
     const size_t rs = sizeof(real);
     const int TR = kp_ >= 64 ? 16 : 32;
-    // tables per launch so the LDS stage fits in 64 KB
-    const int lmax = std::max<int>(1, (int)((64 * 1024 / rs - (size_t)TR * kp_ - TR) / ((size_t)TR * kp_)));
+    // tables per launch so the LDS stage fits in 64 KB (MFMA path: its register budget)
+    const int lmax = mfma_gram(L) ? GRAM_LMAX
+                                  : std::max<int>(1, (int)((64 * 1024 / rs - (size_t)TR * kp_ - TR) / ((size_t)TR * kp_)));
     int l0 = 0;
     bool first = true;
     do {
@@ -1065,10 +1069,21 @@ template <typename real> class Problem final : public ProblemBase {
       uint64_t nbx = std::max<uint64_t>(1, std::min<uint64_t>((Rp + 63) / 64, 512 / gy));
       nbx = std::min<uint64_t>(nbx, std::max<uint64_t>(1, part_.n / nout));
       const uint64_t rpb = (Rp + nbx - 1) / nbx;
-      prof_launch("aggregates", (double)Rp * ((L + (B ? 1 : 0)) * kp_ + (wv ? 1 : 0)) * sizeof(real), [&] {
-        launch(k_gram_part<real, KP, SPT>, dim3((unsigned)nbx, gy), BLOCK, smem, Rp, L, A, B, wv, part_.p,
-                                                                                      rpb, sub_per_y);
-      });
+      const double abytes = (double)Rp * ((L + (B ? 1 : 0)) * kp_ + (wv ? 1 : 0)) * sizeof(real);
+      if (mfma_gram(L)) {  // fp32, KP = 32: the Grams on MFMA (kernels.hpp k_gram_mfma32)
+        nbx = std::max<uint64_t>(1, std::min<uint64_t>((Rp + 127) / 128, 256));
+        nbx = std::min<uint64_t>(nbx, std::max<uint64_t>(1, part_.n / nout));
+        const uint64_t rpbm = (Rp + nbx - 1) / nbx;
+        prof_launch("aggregates", abytes, [&] {
+          launch(k_gram_mfma32<GRAM_LMAX>, (unsigned)nbx, BLOCK, 0, Rp, L, (const float *const *)A, (const float *)B,
+                 (const float *)wv, part_.p, rpbm);
+        });
+      } else {
+        prof_launch("aggregates", abytes, [&] {
+          launch(k_gram_part<real, KP, SPT>, dim3((unsigned)nbx, gy), BLOCK, smem, Rp, L, A, B, wv, part_.p,
+                                                                                        rpb, sub_per_y);
+        });
+      }
       // one reduction launch over [grams -> M (real) | sums -> sums_ (double)]
       const uint64_t ng = (uint64_t)L * KP * KP;
       const uint64_t gm = M ? ng : 0, off = M ? 0 : ng, cnt = gm + (sums ? 2 * KP + 1 : 0);
@@ -1539,6 +1554,7 @@ template <typename real> class Problem final : public ProblemBase {
   uint64_t seg_len_ = 32;
   int lookahead_ = 1;
   int fuse_ = 1;
+  bool no_mfma_ = std::getenv("OCFFM_NO_MFMA") != nullptr;  // Grams on the VALU kernel instead
   bool no_owned_ = false;
   bool owned_stale_ = false;  // owned tables differ across ranks until sync_owned()
   unsigned hs_blocks_ = 4096;  // grid cap of the cross Hessian-vector row pass

@@ -100,6 +100,26 @@ def test_gradient_and_hv_kernels(self_side):
                 assert rel(H1, H0) <= 1e-12, ("hv", f1, f2, half)
 
 
+@pytest.mark.parametrize("env", [{}, {"OCFFM_NO_MFMA": "1"}])
+def test_gradient_and_hv_fp32_k32(monkeypatch, env):
+    """fp32 at k = 32 (the perf build: the cross halves' k x k Grams run on
+    MFMA, kernels.hpp k_gram_mfma32) against the fp64 oracle: every half's
+    gradient and Hessian-vector product within 1e-4 of its largest entry."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    ds = synth.kkbox(seed=5, m=300, n=500, mean=10.0, name="kk_fp32")
+    o, g = pair(ds, precision=ocffm.FP32, with_test=False)
+    rng = np.random.default_rng(3)
+    for f1 in range(o.f):
+        for f2 in range(f1, o.f):
+            for half in (0, 1):
+                G0, G1 = o.grad(f1, f2, half), g.grad(f1, f2, half)
+                assert rel(G1, G0) <= 1e-4, ("grad", f1, f2, half, rel(G1, G0))
+                v = rng.standard_normal(G0.size)
+                H0, H1 = o.hv(f1, f2, half, v), g.hv(f1, f2, half, v)
+                assert rel(H1, H0) <= 1e-4, ("hv", f1, f2, half, rel(H1, H0))
+
+
 def test_block_by_block_fp64(tiny):
     o, g = pair(tiny)
     for f1 in range(o.f):

@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--precision", choices=["fp32", "fp64"], default="fp32")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-epochs", type=int, default=4)
+    ap.add_argument("--sgd", choices=["auto", "off"], default="auto",
+                    help="N=1: also time the SGD/AdaGrad mode (tools/bench_sgd.py) into 'modes'")
     return ap.parse_args()
 
 
@@ -125,7 +127,7 @@ def main():
             "epoch_alg_bytes": alg / max(1, args.steps)}
     # HBM bytes per launch of the same kernel family from the committed
     # rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, MI355X guide §HBM).
-    pmcs = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json")))
+    pmcs = sorted(p for p in glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json")) if "_sgd_" not in p)
     if pmcs:
         pmc = pmcs[-1]
         roof["traffic_source"] = os.path.relpath(pmc, REPO)
@@ -138,6 +140,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
         cpu = cpu_baseline(ds, args.cpu_epochs)
+    modes = None
+    if world == 1 and args.sgd == "auto":
+        modes = {"sgd": sgd_mode(ds, args)}
 
     if rank == 0:
         line = {
@@ -154,10 +159,43 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if modes:
+            line["modes"] = modes
         print(json.dumps(line), flush=True)
     g.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def sgd_mode(ds, args):
+    """The SGD/AdaGrad + on-device-negatives mode on the same kkbox-shape data
+    (north_star extra, parity unpinned vs the reference; tools/bench_sgd.py
+    has the full line).  Instances = positives x 2 (one negative each)."""
+    try:
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        import bench_sgd as BS
+        U = ocffm.ImpData.from_rows(ds.train)
+        V = ocffm.ImpData.from_rows(ds.item)
+        t = ocffm.SgdTrainer(U, V, k=32, nneg=1, neg_power=0.75)
+        t.epoch()
+        t.sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            t.epoch()
+        t.sync()
+        per = (time.perf_counter() - t0) / args.steps
+        info = t.info
+        kp = info["kp"]
+        bpi = BS.slot_rows([0, 1, 1, 2, 3, 4]) * kp * 4 * 4
+        ach = info["instances"] * bpi / per / 1e9
+        t.close()
+        return {"metric": "train instances/sec (SGD/AdaGrad, HOGWILD, on-device negatives)",
+                "value": round(info["instances"] / per, 1), "unit": "instances/s", "ms_per_step": round(per * 1e3, 3),
+                "roofline": {"kernel": "k_sgd", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_instance": bpi},
+                "parity": "unpinned vs reference (no counterpart); pinned to oracle/sgd_oracle.cpp"}
+    except Exception as e:  # never blocks the headline number
+        return {"value": None, "error": str(e)}
 
 
 def cpu_baseline(ds, epochs):

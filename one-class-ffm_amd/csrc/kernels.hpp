@@ -1084,7 +1084,9 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
                                                             const uint32_t *__restrict__ ycol,
                                                             real *__restrict__ yt, const real *__restrict__ Q1,
                                                             uint64_t q1rows, const uint32_t *__restrict__ segd,
-                                                            const real *__restrict__ segx) {
+                                                            const real *__restrict__ segx,
+                                                            real *__restrict__ yt_other,
+                                                            const uint32_t *__restrict__ perm) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP>;
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real));
@@ -1121,17 +1123,26 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
           if ((bt + u) % G::LPR == li) dd[(bt + u) / G::LPR] = d;
         }
       });
-      // each lane owns its positions p0 + li + t*LPR: all loads, then all stores
+      // each lane owns its positions p0 + li + t*LPR: all loads, then all
+      // stores; yt_other: the same new value also stored at the positive's
+      // place in the other orientation (a plain scattered store, no
+      // read-modify-write: both orientations hold the same base)
       real ym[PP::UT];
+      uint32_t pm[PP::UT];
 #pragma unroll
       for (int t = 0; t < PP::UT; t++) {
         const int64_t q = p0 + li + t * G::LPR;
         ym[t] = q < sgm.e ? yt[q] : (real)0;
+        pm[t] = (yt_other && q < sgm.e) ? perm[q] : 0u;
       }
 #pragma unroll
       for (int t = 0; t < PP::UT; t++) {
         const int64_t q = p0 + li + t * G::LPR;
-        if (q < sgm.e) yt[q] = ym[t] + dd[t];
+        if (q < sgm.e) {
+          const real v = ym[t] + dd[t];
+          yt[q] = v;
+          if (yt_other) yt_other[pm[t]] = v;
+        }
       }
     }
   }

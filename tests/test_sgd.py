@@ -117,7 +117,7 @@ PRM = {"eta": 0.2, "lambda": 2e-5, "nneg": 1, "neg_power": 0.75, "adagrad": 1, "
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,adagrad,nneg", [(4, 1, 1), (32, 1, 2), (16, 0, 1)])
+@pytest.mark.parametrize("k,adagrad,nneg", [(4, 1, 1), (32, 1, 2), (16, 0, 1), (64, 1, 1), (100, 1, 0), (1, 1, 3)])
 def test_serial_mode_matches_oracle(k, adagrad, nneg):
     ds = synth.tiny(seed=3, m=300, n=40)
     prm = dict(PRM, adagrad=adagrad, nneg=nneg)

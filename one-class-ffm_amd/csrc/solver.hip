@@ -1076,7 +1076,7 @@ template <typename real> class Problem final : public ProblemBase {
       const uint64_t rpb = (Rp + nbx - 1) / nbx;
       const double abytes = (double)Rp * ((L + (B ? 1 : 0)) * kp_ + (wv ? 1 : 0)) * sizeof(real);
       if (mfma_gram(L)) {  // fp32, KP = 32: the Grams on MFMA (kernels.hpp k_gram_mfma32)
-        nbx = std::max<uint64_t>(1, std::min<uint64_t>((Rp + 127) / 128, 256));
+        nbx = std::max<uint64_t>(1, std::min<uint64_t>((Rp + 127) / 128, gram_blocks_));
         nbx = std::min<uint64_t>(nbx, std::max<uint64_t>(1, part_.n / nout));
         const uint64_t rpbm = (Rp + nbx - 1) / nbx;
         prof_launch("aggregates", abytes, [&] {
@@ -1565,6 +1565,7 @@ template <typename real> class Problem final : public ProblemBase {
   // more than the coalesced gather pass)
   bool scatter_ = std::getenv("OCFFM_SCATTER") != nullptr;
   bool no_mfma_ = std::getenv("OCFFM_NO_MFMA") != nullptr;  // Grams on the VALU kernel instead
+  uint64_t gram_blocks_ = std::getenv("OCFFM_GRAM_BLOCKS") ? std::strtoull(std::getenv("OCFFM_GRAM_BLOCKS"), nullptr, 10) : 256;
   bool no_owned_ = false;
   bool owned_stale_ = false;  // owned tables differ across ranks until sync_owned()
   unsigned hs_blocks_ = 4096;  // grid cap of the cross Hessian-vector row pass

@@ -65,12 +65,21 @@ def main():
 
     ds = synth.kkbox(m=ROWS_PER_GPU * world)
     comm = None
-    if world > 1:
+    allreduce = None
+    rehearsal = world > 1 and os.environ.get("OCFFM_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        # N ranks on one GPU (tests of this script's multi-rank flow on a
+        # one-GPU box): the library's all-reduces go through gloo on the host
+        local = 0
+
+        def allreduce(arr):
+            dist.all_reduce(torch.from_numpy(arr))
+    elif world > 1:
         obj = [ocffm.comm_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         comm = obj[0]
     g = ocffm.problem_from_dataset(ds, precision=prec, with_test=False, device=local, rank=rank, nranks=world,
-                                   comm=comm)
+                                   comm=comm, allreduce=allreduce)
     ocffm.srand(1)
     g.init()
 

@@ -432,8 +432,22 @@ template <typename real> class Problem final : public ProblemBase {
 
   // ------------------------------------------------------------ epoch
   // ffm.cpp:852-870.
+  // OCFFM_TIMING=1: per epoch, host wall time and the part of it the host
+  // spent blocked on the GPU (CG verdict waits).  Blocked most of the time =
+  // GPU-bound; rarely blocked = the host's launch rate is the limit.
+  template <class F> void host_wait(F &&f) {
+    if (!timing_) return f();
+    const auto t = std::chrono::steady_clock::now();
+    f();
+    wait_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+  }
+  bool timing_ = std::getenv("OCFFM_TIMING") != nullptr;
+  double wait_ms_ = 0;
+
   void one_epoch() override {
     need_init();
+    const auto te = std::chrono::steady_clock::now();
+    wait_ms_ = 0;
     if (prm_.self_side) {
       for (uint32_t f1 = 0; f1 < fu_; f1++)
         for (uint32_t f2 = f1; f2 < fu_; f2++) solve_block(f1, f2);
@@ -443,6 +457,13 @@ template <typename real> class Problem final : public ProblemBase {
     for (uint32_t f1 = 0; f1 < fu_; f1++)
       for (uint32_t f2 = fu_; f2 < f_; f2++) solve_block(f1, f2);
     if (prm_.self_side) cache_sasb();
+    if (timing_) {
+      const double host = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - te).count();
+      sync();
+      const double all = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - te).count();
+      std::fprintf(stderr, "[timing] epoch %.3f ms: host enqueue done at %.3f ms, blocked on CG verdicts %.3f ms\n", all,
+                   host, wait_ms_);
+    }
     flush_prof();
   }
 
@@ -1470,12 +1491,12 @@ template <typename real> class Problem final : public ProblemBase {
       evs.push_back(e);
       const int t = it - lookahead_;
       if (t >= 1) {
-        HIPCHK(hipEventSynchronize(evs[t - 1]));
+        host_wait([&] { HIPCHK(hipEventSynchronize(evs[t - 1])); });
         examine(t + 1);  // upd(t) decided run[t+1]
       }
     }
     if (!done) {
-      HIPCHK(hipEventSynchronize(evs.back()));
+      host_wait([&] { HIPCHK(hipEventSynchronize(evs.back())); });
       examine(MAXCG);
     }
     for (auto e : evs) ev_free_.push_back(e);

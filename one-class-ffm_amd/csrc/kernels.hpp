@@ -805,6 +805,21 @@ __global__ __launch_bounds__(BLOCK) void k_hs_side_row(uint64_t R, const int64_t
   const int sg = lane / G::LPR, li = lane % G::LPR;
   double dsum[3] = {0, 0, 0};
   for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
+    if (FUSE) {
+      // id-like field: row i is column d's only row, so the finalisation
+      // operands (p, r, Hp, S of column d) are loaded once and the row's
+      // CG direction is formed from them (V = f.P, Rv = f.R, Hv = f.Hp)
+      const uint32_t d = xidx[i];
+      const real x = xval[i];
+      const FinOps<real> ops = fin_load<real, KP, 1>(f, d, upd, li);
+      const vec_t<real> q = vld<real>(Q1 + i * KP + li * G::VE);
+      vec_t<real> pt = ops.w_or_p;
+      if (upd) pt = (ops.r - vsplat<real>(alpha) * ops.hp) + vsplat<real>(beta) * ops.w_or_p;
+      const real z = sg_sum<G::LPR>(hsum<real>(vsplat<real>(x) * pt * q));
+      const real dd = (real)((1 - w) * (double)(yptr[i + 1] - yptr[i]) + w * n1);
+      col_finalize<real, KP, 1>(f, d, vsplat<real>(x) * (vsplat<real>(dd * z) * q), alpha, beta, upd, li, dsum, ops);
+      continue;
+    }
     vec_t<real> phi = vzero<real>();
     if (one) {  // one node per row: xptr[i] == i
       phi = vsplat<real>(xval[i]) * cg_dir_at<real, KP>(V, Rv, Hv, alpha, beta, upd, (size_t)xidx[i] * KP + li * G::VE);
@@ -815,13 +830,7 @@ __global__ __launch_bounds__(BLOCK) void k_hs_side_row(uint64_t R, const int64_t
     const vec_t<real> q = vld<real>(Q1 + i * KP + li * G::VE);
     const real z = sg_sum<G::LPR>(hsum<real>(phi * q));
     const real d = (real)((1 - w) * (double)(yptr[i + 1] - yptr[i]) + w * n1);
-    const vec_t<real> out = vsplat<real>(d * z) * q;
-    if (!FUSE) {
-      vst<real>(h + i * KP + li * G::VE, out);
-    } else {
-      const int64_t xp = xptr[i];
-      col_finalize<real, KP, 1>(f, xidx[xp], vsplat<real>(xval[xp]) * out, alpha, beta, upd, li, dsum);
-    }
+    vst<real>(h + i * KP + li * G::VE, vsplat<real>(d * z) * q);
   }
   if (FUSE) fin_blocks<real, 1>(f, dsum);
 }

@@ -938,6 +938,160 @@ __global__ __launch_bounds__(BLOCK) void k_hs_cross_seg(uint64_t nseg, const Seg
   if (FUSE) fin_blocks<real, 1>(f, dsum);
 }
 
+// ------------------------------------------- row-complete cross halves ---
+// Id-like field, one GPU, fp32, KP = 32 ("row-complete"): every
+// row is one work unit, so the Hessian-vector row pass finalises its own
+// feature column and no feature pass runs.  Rows with more than HEAVY_POS
+// positives (the Pareto-head items) use their Gram G_i = sum_{j in pos(i)}
+// q_j q_j^T, built once per half, instead of gathering their partner rows
+// every CG step: (1-w) sum_j <phi, q_j> q_j = (1-w) phi G_i.
+constexpr int HEAVY_POS = 32;
+constexpr int GRAM_CHUNK = 1024;  // positives per Gram partial
+#ifndef RC_GB
+#define RC_GB 8  // partner-row gathers per round in k_hs_cross_rc
+#endif
+struct GChunk {
+  uint32_t heavy;  // index of the heavy row
+  uint32_t pad;
+  int64_t b, e;    // positives
+};
+
+// Partial Gram of one chunk of a heavy row's positives on MFMA
+// (v_mfma_f32_32x32x2f32, A = B = the gathered partner rows: lane l loads
+// Q1[ycol[p + l/32]][l%32], a whole 128-B row per half-wave); the block's
+// four waves take interleaved pairs and are combined in wave order.
+static __global__ __launch_bounds__(BLOCK) void k_pos_gram32(const GChunk *__restrict__ chunks,
+                                                            const uint32_t *__restrict__ ycol,
+                                                            const float *__restrict__ Q1, float *__restrict__ gpart) {
+  typedef float f16x __attribute__((ext_vector_type(16)));
+  __shared__ float red[1024];
+  const GChunk c = chunks[blockIdx.x];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, e = lane & 31;
+  f16x acc;
+#pragma unroll
+  for (int r = 0; r < 16; r++) acc[r] = 0.0f;
+  constexpr int U = 4;
+  for (int64_t p0 = c.b + 2 * w; p0 < c.e; p0 += 8 * U) {
+    float a[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t p = p0 + 8 * u + hf;
+      a[u] = p < c.e ? Q1[(size_t)ycol[p] * 32 + e] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], a[u], acc, 0, 0, 0);
+  }
+  for (int ww = 0; ww < BLOCK / 64; ww++) {
+    if (w == ww)
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int m = 8 * (r >> 2) + 4 * hf + (r & 3);
+        float &x = red[m * 32 + e];
+        x = (ww == 0 ? 0.0f : x) + acc[r];
+      }
+    __syncthreads();
+  }
+  for (int t = threadIdx.x; t < 1024; t += BLOCK) gpart[(size_t)blockIdx.x * 1024 + t] = red[t];
+}
+
+// G[h] = sum of heavy row h's chunk partials, in chunk order.
+static __global__ __launch_bounds__(BLOCK) void k_gram_rows(const uint32_t *__restrict__ cptr,
+                                                           const float *__restrict__ gpart, float *__restrict__ G) {
+  const uint32_t h = blockIdx.x, c0 = cptr[h], c1 = cptr[h + 1];
+  for (int t = threadIdx.x; t < 1024; t += BLOCK) {
+    float s = 0;
+    for (uint32_t c = c0; c < c1; c++) s += gpart[(size_t)c * 1024 + t];
+    G[(size_t)h * 1024 + t] = s;
+  }
+}
+
+// Hessian-vector row pass + finalisation of a row-complete cross half
+// (hs_cross, ffm.cpp:715-742, then cg 783-809 for the row's column): one row
+// per subgroup; phi_i = x_i p_t(d_i) from the column's finalisation
+// operands; light rows gather their <= HEAVY_POS partner rows in one round,
+// heavy rows multiply by G_i; + w phi QTQ (QTQ in LDS).
+// x M for a global KP x KP matrix, its rows loaded GROUP at a time (bounded
+// register footprint; sg_vecmat issues all KP row loads at once).
+template <typename real, int KP, int GROUP>
+__device__ __forceinline__ vec_t<real> sg_vecmat_g(const vec_t<real> &x, const real *__restrict__ M, int li) {
+  using G = Geo<real, KP>;
+  vec_t<real> t = vzero<real>();
+#pragma unroll 1
+  for (int e0 = 0; e0 < KP; e0 += GROUP) {
+    vec_t<real> mr[GROUP];
+#pragma unroll
+    for (int u = 0; u < GROUP; u++) mr[u] = vld<real>(M + (size_t)(e0 + u) * KP + li * G::VE);
+    sfor<GROUP>([&](auto U) {
+      constexpr int u = decltype(U)::value;
+      // component e0 + u of x lives in lane (e0 + u) / VE of the subgroup
+      const real xe = __shfl(x[(e0 + u) % G::VE], (int)((threadIdx.x & 63) & ~(G::LPR - 1)) + (e0 + u) / G::VE, 64);
+      t += vsplat<real>(xe) * mr[u];
+    });
+  }
+  return t;
+}
+
+template <int KP>
+__global__ __launch_bounds__(BLOCK) void k_hs_cross_rc(uint64_t R, const int64_t *__restrict__ yptr,
+                                                      const uint32_t *__restrict__ xidx,
+                                                      const float *__restrict__ xval,
+                                                      const uint32_t *__restrict__ ycol, const float *__restrict__ Q1,
+                                                      uint64_t q1rows, const float *__restrict__ QTQ,
+                                                      const uint32_t *__restrict__ hidx, const float *__restrict__ Gh,
+                                                      double w, const int *__restrict__ run, const CgState *st, int it,
+                                                      Fin<float> f) {
+  using G = Geo<float, KP>;
+  using PP = PosPass<float, KP, RC_GB>;
+  static_assert(PP::PW >= HEAVY_POS, "a light row is one pass of PW positions");
+  if (run && !*run) return;
+  __shared__ __align__(16) float Qs[KP * KP];
+  for (int t = threadIdx.x; t < KP * KP; t += BLOCK) Qs[t] = QTQ[t];
+  __syncthreads();
+  const BufView qb = buf_view(Q1, q1rows * KP * sizeof(float));
+  const bool upd = it > 1;
+  const float alpha = upd ? (float)st->alpha : 0.0f, beta = upd ? (float)st->beta : 0.0f;
+  WAVE_SETUP
+  const int sg = lane / G::LPR, li = lane % G::LPR;
+  const float cpos = (float)(1 - w);
+  double dsum[3] = {0, 0, 0};
+  for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
+    const uint32_t d = xidx[i];
+    const float x = xval[i];
+    const int64_t b = yptr[i], e = yptr[i + 1];
+    const uint32_t hv = hidx[i];
+    uint32_t jj[PP::UT];
+    if (hv == 0xffffffffu) PP::load_cols(ycol, b, e, li, jj);
+    const FinOps<float> ops = fin_load<float, KP, 1>(f, d, upd, li);
+    vec_t<float> pt = ops.w_or_p;
+    if (upd) pt = (ops.r - vsplat<float>(alpha) * ops.hp) + vsplat<float>(beta) * ops.w_or_p;
+    const vec_t<float> phi = vsplat<float>(x) * pt;
+    vec_t<float> ka = vzero<float>();
+    if (hv != 0xffffffffu) {
+      ka = sg_vecmat_g<float, KP, 8>(phi, Gh + (size_t)hv * KP * KP, li);
+    } else if (e > b) {
+      sfor<PP::PW / PP::GB>([&](auto BT) {  // GB gathers per round
+        constexpr int bt = decltype(BT)::value * PP::GB;
+        if (b + bt >= e) return;
+        vec_t<float> qv[PP::GB];
+        sfor<PP::GB>([&](auto U) {
+          constexpr int u = decltype(U)::value;
+          qv[u] = bld<float>(qb, PP::row_off(PP::template at<bt + u>(jj, li), qb, li));
+        });
+        float dv[PP::GB];
+#pragma unroll
+        for (int u = 0; u < PP::GB; u++) dv[u] = sg_sum<G::LPR>(hsum<float>(phi * qv[u]));
+#pragma unroll
+        for (int u = 0; u < PP::GB; u++) ka += vsplat<float>(dv[u]) * qv[u];
+      });
+    }
+    // (grouped: the fully unrolled sg_vecmat hoists all KP LDS row loads and
+    // doubles the kernel's registers: 256 -> ~130 VGPRs)
+    const vec_t<float> hvec = vsplat<float>(cpos) * ka + vsplat<float>((float)w) * sg_vecmat_g<float, KP, 8>(phi, Qs, li);
+    col_finalize<float, KP, 1>(f, d, vsplat<float>(x) * hvec, alpha, beta, upd, li, dsum, ops);
+  }
+  fin_blocks<float, 1>(f, dsum);
+}
+
 // ------------------------------------------------------ feature pass ---
 // acc_col = sum_{(r, x) in column} x h[r] for every feature column of a field
 // (the X^T h of gd_* / hs_*, ffm.cpp:561-570, 603-624, 715-742), then

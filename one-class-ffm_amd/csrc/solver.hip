@@ -121,7 +121,38 @@ template <typename real> struct DevSide {
   uint64_t nseg = 0;      // positive segments (kernels.hpp: Seg)
   DevBuf<Seg> segs;
   DevBuf<uint32_t> segptr;
+  // row-complete cross halves (kernels.hpp k_hs_cross_rc): heavy rows (more
+  // than HEAVY_POS positives) and the chunks of their Gram build
+  uint64_t nheavy = 0, nchunk = 0, heavy_pos = 0;
+  DevBuf<uint32_t> hidx;   // R: heavy index or ~0
+  DevBuf<GChunk> chunks;
+  DevBuf<uint32_t> cptr;   // nheavy + 1
+  DevBuf<float> gpart, gram;
 };
+
+// Heavy rows of a side and their Gram chunks (row-complete cross halves).
+template <typename real> static void build_heavy(DevSide<real> &s, const std::vector<int64_t> &yptr) {
+  const uint64_t R = yptr.size() - 1;
+  std::vector<uint32_t> hidx(std::max<uint64_t>(R, 1), 0xffffffffu), cptr{0};
+  std::vector<GChunk> ch;
+  for (uint64_t i = 0; i < R; i++) {
+    const int64_t b = yptr[i], e = yptr[i + 1];
+    if (e - b <= HEAVY_POS) continue;
+    hidx[i] = (uint32_t)s.nheavy++;
+    s.heavy_pos += (uint64_t)(e - b);
+    for (int64_t p = b; p < e; p += GRAM_CHUNK)
+      ch.push_back(GChunk{hidx[i], 0u, p, std::min<int64_t>(e, p + GRAM_CHUNK)});
+    cptr.push_back((uint32_t)ch.size());
+  }
+  s.nchunk = ch.size();
+  s.hidx.upload(hidx);
+  s.chunks.upload(ch.empty() ? std::vector<GChunk>{GChunk{0, 0, 0, 0}} : ch);
+  s.cptr.upload(cptr);
+  if (std::is_same<real, float>::value && s.nheavy) {
+    s.gpart.alloc(s.nchunk * 1024, false);
+    s.gram.alloc(s.nheavy * 1024, false);
+  }
+}
 
 // Split every row's positives into segments of at most `len` (rows without
 // positives still get one, empty, segment for their row-local terms).
@@ -686,6 +717,7 @@ template <typename real> class Problem final : public ProblemBase {
       aggregates(hc.partner->R, (int)C_, partner_tabs(hc), hc.Q1, nullptr, M_.p);
       const uint32_t c0 = cross_slot(std::min(hc.fl, hc.fo), std::max(hc.fl, hc.fo));
       qtq_ = M_.p + (size_t)c0 * kp_ * kp_;
+      heavy_grams(hc);
     }
     // force iteration 1 to run
     CgState hs{};
@@ -844,6 +876,7 @@ template <typename real> class Problem final : public ProblemBase {
     for (uint64_t p = pb; p < pe; p++) ycol[p - pb] = (uint32_t)U.ycol[p];
     U_.npos = pe - pb;
     build_segments(U_, yptr, seg_len_, nsg());
+    build_heavy(U_, yptr);
     U_.yptr.upload(yptr);
     U_.ycol.upload(ycol);
     U_.yt.alloc(std::max<uint64_t>(U_.npos, 1));
@@ -876,6 +909,7 @@ template <typename real> class Problem final : public ProblemBase {
       }
     V_.npos = np;
     build_segments(V_, vptr, seg_len_, nsg());
+    build_heavy(V_, vptr);
     V_.yptr.upload(vptr);
     V_.ycol.upload(vcol);
     V_.yt.alloc(std::max<uint64_t>(np, 1));
@@ -1329,6 +1363,28 @@ template <typename real> class Problem final : public ProblemBase {
     return f;
   }
   // id-like field on one GPU: the row pass finalises its feature column.
+  // The heavy rows' Grams G_i = sum_j q_j q_j^T of a row-complete half (its
+  // partner rows q_j are fixed for the whole CG solve).
+  void heavy_grams(const HalfCtx &h) {
+    if (!row_complete(h) || !h.own->nheavy) return;
+    DevSide<real> &own = *h.own;
+    prof_launch("heavy_gram", (double)own.heavy_pos * (4 + 128) + own.nchunk * 4096.0 * 2, [&] {
+      launch(k_pos_gram32, (unsigned)own.nchunk, BLOCK, 0, (const GChunk *)own.chunks.p, (const uint32_t *)own.ycol.p,
+             (const float *)h.Q1, (float *)own.gpart.p);
+      launch(k_gram_rows, (unsigned)own.nheavy, BLOCK, 0, (const uint32_t *)own.cptr.p, (const float *)own.gpart.p,
+             (float *)own.gram.p);
+    });
+  }
+
+  // Row-complete cross half (kernels.hpp k_hs_cross_rc): fp32 at KP = 32,
+  // one GPU, id-like field, and the heavy rows' Grams cheap to build (at most
+  // a quarter of the side's positives in heavy rows: the items, whose heavy
+  // rows are the Pareto head; not the users, most of whom are heavy).
+  bool row_complete(const HalfCtx &h) const {
+    return std::is_same<real, float>::value && kp_ == 32 && h.cross && h.F->idlike && !comm_.active() && rc_ &&
+           h.own->heavy_pos * 4 <= h.own->npos;
+  }
+
   // fuse_ 1: the Hessian-vector pass of side halves only (one row = one
   // feature, no partial sums); 2: every row pass (the gradient passes and the
   // cross halves walk positive segments, whose multi-segment rows meet through
@@ -1411,6 +1467,22 @@ template <typename real> class Problem final : public ProblemBase {
   void hv_pass(HalfCtx &h, int it) {
     DevSide<real> &own = *h.own;
     const int *run = &st_.p->run[it];
+    if (row_complete(h)) {
+      if constexpr (std::is_same<real, float>::value) {
+        DevField<real> &F = *h.F;
+        const Fin<real> fin = make_fin(h, it);
+        const double rs = sizeof(real);
+        const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)own.npos * 4 +
+                             (double)h.partner->R * 32 * rs + (double)own.nheavy * 4096 + (double)F.D * 32 * rs * 8;
+        prof_launch("hs_cross_rc", bytes, [&] {
+          launch(k_hs_cross_rc<32>, grid_for(own.R, 4 * Geo<float, 32>::NSG, 2048), BLOCK, 0, (uint64_t)own.R,
+                 (const int64_t *)own.yptr.p, (const uint32_t *)F.xidx.p, (const float *)F.xval.p,
+                 (const uint32_t *)own.ycol.p, (const float *)h.Q1, (uint64_t)h.partner->R, (const float *)qtq_,
+                 (const uint32_t *)own.hidx.p, (const float *)own.gram.p, w_, run, (const CgState *)st_.p, it, fin);
+        });
+      }
+      return;
+    }
     const bool fz_ = fused_rows(h, true);
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
@@ -1470,6 +1542,7 @@ template <typename real> class Problem final : public ProblemBase {
       HIPCHK(hipEventRecord(hb, stream_));
     }
     gradient(h);
+    heavy_grams(h);
     // CG with `lookahead_` iterations in flight (see file header): iteration
     // it is enqueued before the host waits for iteration it-L's verdict, so
     // the GPU never waits on the host.  Iterations past the real exit run as
@@ -1580,6 +1653,12 @@ template <typename real> class Problem final : public ProblemBase {
   uint64_t seg_len_ = 32;
   int lookahead_ = 1;
   int fuse_ = 1;
+  // OCFFM_RC=1: row-complete id-field cross halves (k_hs_cross_rc).  Correct
+  // (tests) but measured slower at kkbox shape: 57 us per CG step against
+  // 25 + 15 us for the segment row pass + feature pass (its light rows take
+  // four gather rounds at the register budget of 3 waves/SIMD, where the
+  // segment pass issues all 32 gathers at once at 4 waves/SIMD).
+  bool rc_ = std::getenv("OCFFM_RC") != nullptr;
   // OCFFM_SCATTER=1: the cross update also writes the other orientation of
   // base by scattered 4-B stores instead of the gather kernel k_gather_pos
   // (measured 2 % slower per epoch: the scattered partial-line writes cost

@@ -100,14 +100,18 @@ def test_gradient_and_hv_kernels(self_side):
                 assert rel(H1, H0) <= 1e-12, ("hv", f1, f2, half)
 
 
-@pytest.mark.parametrize("env", [{}, {"OCFFM_NO_MFMA": "1"}])
+KK_RC = dict(seed=3, m=1500, n=4000, mean=20.0, name="kk_rc")  # ~24 % heavy positives on both sides
+
+
+@pytest.mark.parametrize("env", [{}, {"OCFFM_NO_MFMA": "1"}, {"OCFFM_RC": "1"}])
 def test_gradient_and_hv_fp32_k32(monkeypatch, env):
-    """fp32 at k = 32 (the perf build: the cross halves' k x k Grams run on
-    MFMA, kernels.hpp k_gram_mfma32) against the fp64 oracle: every half's
+    """fp32 at k = 32 (the perf build: the cross halves' k x k Grams on MFMA,
+    kernels.hpp k_gram_mfma32; the id-field cross halves row-complete with
+    heavy-row Grams, k_hs_cross_rc, opt-in) against the fp64 oracle: every half's
     gradient and Hessian-vector product within 1e-4 of its largest entry."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
-    ds = synth.kkbox(seed=5, m=300, n=500, mean=10.0, name="kk_fp32")
+    ds = synth.kkbox(**KK_RC)
     o, g = pair(ds, precision=ocffm.FP32, with_test=False)
     rng = np.random.default_rng(3)
     for f1 in range(o.f):
@@ -118,6 +122,26 @@ def test_gradient_and_hv_fp32_k32(monkeypatch, env):
                 v = rng.standard_normal(G0.size)
                 H0, H1 = o.hv(f1, f2, half, v), g.hv(f1, f2, half, v)
                 assert rel(H1, H0) <= 1e-4, ("hv", f1, f2, half, rel(H1, H0))
+
+
+@pytest.mark.parametrize("env", [{}, {"OCFFM_RC": "1"}])
+def test_epochs_fp32_k32_row_complete(monkeypatch, env):
+    """Two fp32 epochs at k = 32 with the row-complete id-field cross halves
+    (OCFFM_RC=1) and without: objective of the fp32 state (evaluated in fp64) within
+    1e-3 of the oracle's; CG counts within 1 per half."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    ds = synth.kkbox(**KK_RC)
+    o, g = pair(ds, precision=ocffm.FP32, with_test=False)
+    for _ in range(2):
+        o.one_epoch()
+        g.one_epoch()
+    f_ref = o.func()
+    o2 = O.Oracle(ds, with_test=False)
+    ocffm.srand(1)
+    o2.init()
+    assert abs(gpu_objective(o2, g) - f_ref) <= 1e-3 * abs(f_ref)
+    assert np.abs(g.cg_log().astype(int) - o.cg_log().astype(int)).max() <= 1
 
 
 def test_block_by_block_fp64(tiny):

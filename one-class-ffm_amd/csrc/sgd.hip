@@ -413,7 +413,7 @@ class Trainer {
         block = 64;
       } else {
         block = 256;
-        grid = (unsigned)std::min<uint64_t>((T_ + 3) / 4, 2048);
+        grid = (unsigned)std::min<uint64_t>((T_ + 3) / 4, grid_cap_);
       }
       const int smax = smax_;
       launch_kp([&](auto K) {
@@ -605,6 +605,8 @@ class Trainer {
   uint32_t kp_ = 4, fu_ = 0, fv_ = 0, F_ = 0;
   int smax_ = 1;  // slot rows per wave in LDS: max nodes x fields
   int spg_ = 2;   // slots per subgroup of the k_sgd instantiation
+  // blocks per epoch launch (grid-stride over the instances); OCFFM_SGD_GRID overrides
+  uint64_t grid_cap_ = std::getenv("OCFFM_SGD_GRID") ? std::max<uint64_t>(1, std::strtoull(std::getenv("OCFFM_SGD_GRID"), nullptr, 10)) : 2048;
   bool occ4_ = std::getenv("OCFFM_SGD_OCC") == nullptr || std::atoi(std::getenv("OCFFM_SGD_OCC")) != 0;
   uint64_t nf_ = 0, P_ = 0, T_ = 0, n_items_ = 0, epoch_ = 0, last_A_ = 1, last_B_ = 0;
   uint64_t h_uptr_size_ = 0, h_vptr_size_ = 0;

@@ -605,8 +605,10 @@ class Trainer {
   uint32_t kp_ = 4, fu_ = 0, fv_ = 0, F_ = 0;
   int smax_ = 1;  // slot rows per wave in LDS: max nodes x fields
   int spg_ = 2;   // slots per subgroup of the k_sgd instantiation
-  // blocks per epoch launch (grid-stride over the instances); OCFFM_SGD_GRID overrides
-  uint64_t grid_cap_ = std::getenv("OCFFM_SGD_GRID") ? std::max<uint64_t>(1, std::strtoull(std::getenv("OCFFM_SGD_GRID"), nullptr, 10)) : 2048;
+  // blocks per epoch launch (grid-stride over the instances); OCFFM_SGD_GRID overrides.
+  // Measured at kkbox shape, k=32 (tools/sgd_grid.sh, M instances/s): 512: 236, 1024: 395,
+  // 2048: 398, 8192: 406, 32768: 411, 131072: 403, one block per 4 instances: 82
+  uint64_t grid_cap_ = std::getenv("OCFFM_SGD_GRID") ? std::max<uint64_t>(1, std::strtoull(std::getenv("OCFFM_SGD_GRID"), nullptr, 10)) : 32768;
   bool occ4_ = std::getenv("OCFFM_SGD_OCC") == nullptr || std::atoi(std::getenv("OCFFM_SGD_OCC")) != 0;
   uint64_t nf_ = 0, P_ = 0, T_ = 0, n_items_ = 0, epoch_ = 0, last_A_ = 1, last_B_ = 0;
   uint64_t h_uptr_size_ = 0, h_vptr_size_ = 0;

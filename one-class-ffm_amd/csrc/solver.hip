@@ -327,6 +327,7 @@ template <typename real> class Problem final : public ProblemBase {
     if (const char *e = std::getenv("OCFFM_SEG_LEN")) seg_len_ = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
     if (const char *e = std::getenv("OCFFM_LOOKAHEAD")) lookahead_ = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("OCFFM_HS_BLOCKS")) hs_blocks_ = (unsigned)std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("OCFFM_FEAT_BLOCKS")) feat_blocks_ = (unsigned)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("OCFFM_FUSE")) fuse_ = std::atoi(e);  // id-field row fusion: 0 off, 1 side, 2 all
     if (const char *e = std::getenv("OCFFM_NO_OWNED")) no_owned_ = std::atoi(e) != 0;  // all-reduce every field
     // shard users contiguously
@@ -1414,7 +1415,7 @@ template <typename real> class Problem final : public ProblemBase {
       const double vecs = mode == 2 ? 1 : (mode == 0 ? 5 : (it > 1 ? 8 : 3));
       const double bytes = (double)ent * (4 + rs) + (double)ent * KP * rs + (double)njw * Gm::NSG * sizeof(Job) +
                            (double)h.D * KP * rs * vecs;
-      const unsigned grid = (unsigned)std::min<uint64_t>((njw + 3) / 4, 1024);  // grid-stride: fewer tickets
+      const unsigned grid = (unsigned)std::min<uint64_t>((njw + 3) / 4, feat_blocks_);  // grid-stride: fewer tickets
       const Fin<real> fin = make_fin(h, it);
       const Job *jobs = seg ? F.sjobs.p : F.jobs.p;
       const uint32_t *crow = seg ? F.scrow.p : F.crow.p;
@@ -1669,6 +1670,7 @@ template <typename real> class Problem final : public ProblemBase {
   bool no_owned_ = false;
   bool owned_stale_ = false;  // owned tables differ across ranks until sync_owned()
   unsigned hs_blocks_ = 4096;  // grid cap of the cross Hessian-vector row pass
+  unsigned feat_blocks_ = 1024;  // grid cap of the feature pass (grid-stride over jobs)
   hipEvent_t arm_a_ = nullptr, arm_b_ = nullptr;
   bool arm_first_ = false;
   DevSide<real> U_, V_, T_;

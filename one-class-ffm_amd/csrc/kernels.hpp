@@ -48,6 +48,14 @@ template <typename real, int KP> struct Geo {
 };
 
 constexpr int BLOCK = 256;   // 4 waves
+// Minimum waves per SIMD the positive-gather row passes are compiled for
+// (1 = the compiler's choice); experiment builds set them with -D.
+#ifndef OCFFM_HS_OCC
+#define OCFFM_HS_OCC 1
+#endif
+#ifndef OCFFM_GD_OCC
+#define OCFFM_GD_OCC 1
+#endif
 constexpr int MAXCG = 20;    // ffm.cpp:761
 constexpr double CG_EPS = 9e-2;  // ffm.cpp:762
 
@@ -648,7 +656,7 @@ __global__ __launch_bounds__(BLOCK) void k_init_ytilde(uint64_t R, const int64_t
 // the CSC is the identity, so instead of writing h the kernel finalises the
 // row's feature column itself (col_arrive / col_finalize, MODE 0).
 template <typename real, int KP, bool MLDS, bool FUSE>
-__global__ __launch_bounds__(BLOCK) void k_gd_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
+__global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                         const uint32_t *__restrict__ ycol,
                                                         const real *__restrict__ yt, const real *__restrict__ Q1,
                                                         int C, const real *const *__restrict__ Ptabs,
@@ -840,7 +848,7 @@ __global__ __launch_bounds__(BLOCK) void k_hs_side_row(uint64_t R, const int64_t
 // tau = X_i (V QTQ) = phi_i QTQ).  QTQ staged in LDS; phi_i's components
 // are broadcast by DPP for the k x k product (sg_vecmat).
 template <typename real, int KP, bool MLDS, bool FUSE>
-__global__ __launch_bounds__(BLOCK) void k_hs_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
+__global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                         const int64_t *__restrict__ xptr,
                                                         const uint32_t *__restrict__ xidx,
                                                         const real *__restrict__ xval, const real *__restrict__ V,

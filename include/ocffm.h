@@ -241,6 +241,10 @@ int ocffm_sgd_create(const ocffm_data *U, const ocffm_data *V, const ocffm_sgd_p
  * (RCCL all-reduce over xGMI) — periodic model averaging. */
 int ocffm_sgd_create_dist(const ocffm_data *U, const ocffm_data *V, const ocffm_sgd_param *p, int rank, int nranks,
                           const void *comm_id, ocffm_sgd **out);
+/* The same with ocffm_sgd_average's sums staged through host memory and
+ * handed to fn (float arrays: W, then G) — tests of the sharding on one GPU. */
+int ocffm_sgd_create_dist_host(const ocffm_data *U, const ocffm_data *V, const ocffm_sgd_param *p, int rank,
+                               int nranks, ocffm_allreduce_fn fn, void *user, ocffm_sgd **out);
 int ocffm_sgd_epoch(ocffm_sgd *s, double *mean_loss);
 int ocffm_sgd_average(ocffm_sgd *s);
 /* phi for n (user row, item row) pairs with the current W. */

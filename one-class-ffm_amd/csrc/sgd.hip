@@ -306,8 +306,9 @@ namespace sgd {
 // ---------------------------------------------------------------- host
 class Trainer {
  public:
-  Trainer(const HostData &U, const HostData &V, const ocffm_sgd_param &prm, int rank, int nranks, const void *cid)
-      : prm_(prm), rank_(rank), nranks_(nranks) {
+  Trainer(const HostData &U, const HostData &V, const ocffm_sgd_param &prm, int rank, int nranks, const void *cid,
+          ocffm_allreduce_fn host_fn = nullptr, void *host_user = nullptr)
+      : prm_(prm), rank_(rank), nranks_(nranks), host_fn_(host_fn), host_user_(host_user) {
     if (prm.k == 0 || prm.k > 128) throw Error(OCFFM_E_ARG, "k must be in 1..128");
     if (nranks < 1 || rank < 0 || rank >= nranks) throw Error(OCFFM_E_ARG, "bad rank / nranks");
     int ndev = 0;
@@ -377,7 +378,7 @@ class Trainer {
     W_.upload(W);
     G_.upload(G);
     loss_.alloc(1);
-    if (nranks > 1) {
+    if (cid && !host_fn_) {  // a one-rank communicator too (tests of the RCCL path)
       ncclUniqueId id;
       std::memcpy(&id, cid, sizeof(id));
       NCCLCHK(ncclCommInitRank(&nccl_, nranks, id, rank));
@@ -440,11 +441,22 @@ class Trainer {
   }
 
   // Model averaging over the ranks: W, G <- mean over ranks (RCCL).
+  // With a host hook (tests on one GPU) the sums go through host memory.
   void average() {
-    if (!nccl_) return;
+    if (!nccl_ && !host_fn_) return;
     const size_t nw = (size_t)nf_ * F_ * kp_;
-    NCCLCHK(ncclAllReduce(W_.p, W_.p, nw, ncclFloat, ncclSum, nccl_, stream_));
-    NCCLCHK(ncclAllReduce(G_.p, G_.p, nw, ncclFloat, ncclSum, nccl_, stream_));
+    if (host_fn_) {
+      std::vector<float> hb(nw);
+      for (float *dp : {W_.p, G_.p}) {
+        HIPCHK(hipMemcpyAsync(hb.data(), dp, nw * sizeof(float), hipMemcpyDeviceToHost, stream_));
+        HIPCHK(hipStreamSynchronize(stream_));
+        if (host_fn_(hb.data(), nw, 0, host_user_) != 0) throw Error(OCFFM_E_HIP, "host all-reduce failed");
+        HIPCHK(hipMemcpyAsync(dp, hb.data(), nw * sizeof(float), hipMemcpyHostToDevice, stream_));
+      }
+    } else {
+      NCCLCHK(ncclAllReduce(W_.p, W_.p, nw, ncclFloat, ncclSum, nccl_, stream_));
+      NCCLCHK(ncclAllReduce(G_.p, G_.p, nw, ncclFloat, ncclSum, nccl_, stream_));
+    }
     const float s = 1.0f / (float)nranks_;
     hipLaunchKernelGGL(k_scale, 2048, 256, 0, stream_, (uint64_t)nw, W_.p, s);
     hipLaunchKernelGGL(k_scale, 2048, 256, 0, stream_, (uint64_t)nw, G_.p, s);
@@ -600,6 +612,8 @@ class Trainer {
 
   ocffm_sgd_param prm_;
   int rank_, nranks_;
+  ocffm_allreduce_fn host_fn_ = nullptr;
+  void *host_user_ = nullptr;
   hipStream_t stream_ = nullptr;
   ncclComm_t nccl_ = nullptr;
   uint32_t kp_ = 4, fu_ = 0, fv_ = 0, F_ = 0;
@@ -644,12 +658,12 @@ void ocffm_sgd_param_default(ocffm_sgd_param *p) {
 }
 
 static int sgd_create(const ocffm_data *U, const ocffm_data *V, const ocffm_sgd_param *p, int rank, int nranks,
-                      const void *cid, ocffm_sgd **out) {
+                      const void *cid, ocffm_sgd **out, ocffm_allreduce_fn fn = nullptr, void *user = nullptr) {
   return guarded([&] {
     if (!U || !V || !p || !out) throw ocffm::Error(OCFFM_E_ARG, "null argument");
     if (!U->d.has_label) throw ocffm::Error(OCFFM_E_ARG, "training data without labels");
     auto s = std::make_unique<ocffm_sgd>();
-    s->t = std::make_unique<ocffm::sgd::Trainer>(U->d, V->d, *p, rank, nranks, cid);
+    s->t = std::make_unique<ocffm::sgd::Trainer>(U->d, V->d, *p, rank, nranks, cid, fn, user);
     *out = s.release();
   });
 }
@@ -661,6 +675,12 @@ int ocffm_sgd_create_dist(const ocffm_data *U, const ocffm_data *V, const ocffm_
                           const void *comm_id, ocffm_sgd **out) {
   if (!comm_id && nranks > 1) return guarded([] { throw ocffm::Error(OCFFM_E_ARG, "comm_id required"); });
   return sgd_create(U, V, p, rank, nranks, comm_id, out);
+}
+
+int ocffm_sgd_create_dist_host(const ocffm_data *U, const ocffm_data *V, const ocffm_sgd_param *p, int rank,
+                               int nranks, ocffm_allreduce_fn fn, void *user, ocffm_sgd **out) {
+  if (!fn) return guarded([] { throw ocffm::Error(OCFFM_E_ARG, "all-reduce hook required"); });
+  return sgd_create(U, V, p, rank, nranks, nullptr, out, fn, user);
 }
 
 #define SGD_CALL(body)                                                  \

@@ -68,7 +68,7 @@ EXPORTS = [
     "ocffm_problem_kernel_stats",
     "ocffm_problem_reset_stats", "ocffm_problem_alg_bytes", "ocffm_problem_sync",
     "ocffm_problem_destroy",
-    "ocffm_sgd_param_default", "ocffm_sgd_create", "ocffm_sgd_create_dist", "ocffm_sgd_epoch",
+    "ocffm_sgd_param_default", "ocffm_sgd_create", "ocffm_sgd_create_dist", "ocffm_sgd_create_dist_host", "ocffm_sgd_epoch",
     "ocffm_sgd_average", "ocffm_sgd_phi", "ocffm_sgd_get", "ocffm_sgd_set_w", "ocffm_sgd_get_info",
     "ocffm_sgd_sync", "ocffm_sgd_destroy",
 ]
@@ -123,6 +123,7 @@ def lib():
     L.ocffm_sgd_param_default.restype = None
     L.ocffm_sgd_create.argtypes = [vp, vp, vp, C.POINTER(vp)]
     L.ocffm_sgd_create_dist.argtypes = [vp, vp, vp, i32, i32, vp, C.POINTER(vp)]
+    L.ocffm_sgd_create_dist_host.argtypes = [vp, vp, vp, i32, i32, ALLREDUCE_FN, vp, C.POINTER(vp)]
     L.ocffm_sgd_epoch.argtypes = [vp, C.POINTER(dbl)]
     L.ocffm_sgd_average.argtypes = [vp]
     L.ocffm_sgd_phi.argtypes = [vp, u64, vp, vp, vp]
@@ -263,7 +264,7 @@ class SgdTrainer:
     oracle/sgd_oracle.cpp, not the reference."""
 
     def __init__(self, U: "ImpData", V: "ImpData", rank: int = 0, nranks: int = 1, comm: Optional[bytes] = None,
-                 **kw):
+                 allreduce=None, **kw):
         p = _SgdParam()
         lib().ocffm_sgd_param_default(C.byref(p))
         for key, val in kw.items():
@@ -271,7 +272,16 @@ class SgdTrainer:
         self.param = p
         self._keep = (U, V)
         h = C.c_void_p()
-        if nranks > 1 or comm is not None:
+        if allreduce is not None:  # average() through a host all-reduce (float32 arrays)
+            def cb(buf, count, is_double, user):
+                try:
+                    allreduce(np.ctypeslib.as_array(C.cast(buf, C.POINTER(C.c_float)), shape=(count,)))
+                    return 0
+                except Exception:  # pragma: no cover
+                    return 1
+            self._cb = ALLREDUCE_FN(cb)
+            _check(lib().ocffm_sgd_create_dist_host(U.h, V.h, C.byref(p), rank, nranks, self._cb, None, C.byref(h)))
+        elif nranks > 1 or comm is not None:
             idb = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(comm)
             _check(lib().ocffm_sgd_create_dist(U.h, V.h, C.byref(p), rank, nranks, idb, C.byref(h)))
         else:

@@ -178,3 +178,85 @@ def test_hogwild_trains_like_serial():
     ls = [ser.epoch() for _ in range(3)]
     assert lh[2] < lh[0] and ls[2] < ls[0], (lh, ls)
     assert abs(lh[2] - ls[2]) <= 0.05 * ls[2], (lh, ls)
+
+
+@pytest.mark.gpu
+def test_rccl_one_rank_average_is_identity():
+    """The RCCL averaging path (ncclAllReduce of W and G, scale by 1/N) on a
+    one-rank communicator leaves the serial run's state bit-identical."""
+    import ocffm
+    ds = synth.tiny(seed=3, m=300, n=40)
+    a = _trainer(ds, k=16, serial=1, **PRM)
+    U = ocffm.ImpData.from_rows(ds.train)
+    V = ocffm.ImpData.from_rows(ds.item)
+    b = ocffm.SgdTrainer(U, V, rank=0, nranks=1, comm=ocffm.comm_id(), k=16, serial=1, **PRM)
+    for _ in range(2):
+        assert a.epoch() == b.epoch()
+        b.average()
+    np.testing.assert_array_equal(a.get("W"), b.get("W"))
+    np.testing.assert_array_equal(a.get("G"), b.get("G"))
+
+
+def _sgd_worker(rank, port, out_dir, world):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import ocffm
+
+    def allreduce(arr):
+        dist.all_reduce(torch.from_numpy(arr))
+
+    ds = synth.tiny(seed=3, m=300, n=40)
+    U = ocffm.ImpData.from_rows(ds.train)
+    V = ocffm.ImpData.from_rows(ds.item)
+    t = ocffm.SgdTrainer(U, V, rank=rank, nranks=world, allreduce=allreduce, k=16, serial=1, **PRM)
+    W0, G0 = t.get("W").copy(), t.get("G").copy()
+    loss = t.epoch()
+    W1, G1, o = t.get("W").copy(), t.get("G").copy(), t.get("o").copy()
+    t.average()
+    np.savez(os.path.join(out_dir, f"s{rank}.npz"), W0=W0, G0=G0, W1=W1, G1=G1, o=o, loss=loss,
+             Wa=t.get("W"), Ga=t.get("G"), inst=t.info["instances"])
+    t.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_rank_shards_match_oracle_and_average():
+    """Two ranks on one GPU (host all-reduce hook over gloo): each rank's
+    epoch over its contiguous user shard matches the serial oracle on that
+    shard's positives, and average() leaves the mean of the two models."""
+    import socket
+    import tempfile
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    world = 2
+    ds = synth.tiny(seed=3, m=300, n=40)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_sgd_worker, args=(port, d, world), nprocs=world, join=True)
+        res = [dict(np.load(os.path.join(d, f"s{r}.npz"))) for r in range(world)]
+    m = ds.train.m
+    assert sum(int(r["inst"]) for r in res) == int(ds.train.yptr[-1]) * (1 + PRM["nneg"])
+    for rank, r in enumerate(res):
+        np.testing.assert_array_equal(r["W0"], res[0]["W0"])  # same initial model on every rank
+        o = OracleSgd(ds, None, None, PRM)
+        u0, u1 = m * rank // world, m * (rank + 1) // world
+        keep = (o.pu >= u0) & (o.pu < u1)
+        o.pu, o.pv = np.ascontiguousarray(o.pu[keep]), np.ascontiguousarray(o.pv[keep])
+        F = int(ds.train.fid.max()) + 1 + int(ds.item.fid.max()) + 1
+        o.F, o.kp = F, 16
+        W, G = r["W0"].copy(), r["G0"].copy()
+        A, B, T = (int(x) for x in r["o"])
+        assert T == o.pu.size * (1 + PRM["nneg"])
+        lo = o.epoch(W, G, 0, A, B) / T
+        assert np.abs(r["W1"] - W).max() <= 2e-4 * np.abs(W).max()
+        assert abs(float(r["loss"]) - lo) <= 1e-4 * abs(lo)
+        np.testing.assert_allclose(r["G1"], G, rtol=1e-3, atol=1e-6)
+    mean_w = (res[0]["W1"] + res[1]["W1"]) * np.float32(0.5)
+    mean_g = (res[0]["G1"] + res[1]["G1"]) * np.float32(0.5)
+    for r in res:
+        np.testing.assert_allclose(r["Wa"], mean_w, rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(r["Ga"], mean_g, rtol=1e-6, atol=1e-7)

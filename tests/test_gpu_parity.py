@@ -186,13 +186,25 @@ def test_epochs_fp32_tiny(tiny):
     assert abs(f32obj - f_ref) <= 1e-3 * abs(f_ref)
 
 
-@pytest.mark.parametrize("variant", ["ns", "freq", "k5", "k16", "multi_nnz", "k1", "k64", "k100", "sparse"])
+@pytest.mark.parametrize("variant", ["ns", "freq", "k5", "k16", "multi_nnz", "k1", "k64", "k100", "sparse",
+                                     "kdd12", "outbrain", "wide_ns"])
 def test_variants_fp64(variant):
     """Flags and shapes: --ns, --freq, k = 1 / 5 / 16 / 64 / 100 (padded rows of
-    4 .. 128: one to 64 lanes per row), several nodes per field, and a sparse
-    set (users and items without positives, empty feature columns)."""
+    4 .. 128: one to 64 lanes per row), several nodes per field, a sparse
+    set (users and items without positives, empty feature columns), and the
+    field structures of BASELINE configs 2, 4 and 5 at test size:
+    kdd12-shape (fu=2, fv=4, k=16), outbrain-shape (fu=2, fv=2, k=64, ~1
+    positive per row) and the wide --ns set (fu=39, fv=1: 39 cross blocks)."""
     kw = {}
-    if variant == "multi_nnz":
+    if variant == "kdd12":
+        ds = synth.general(seed=31, m=400, n=120, fu=2, fv=4, k=16, mean_pos=3.0, test_rows=40, name="kdd12")
+    elif variant == "outbrain":
+        ds = synth.general(seed=32, m=400, n=60, fu=2, fv=2, k=64, mean_pos=1.0, test_rows=40, name="outbrain")
+        kw["k"] = 64
+    elif variant == "wide_ns":
+        ds = synth.general(seed=33, m=200, n=40, fu=39, fv=1, k=8, d_user=[20] * 39, d_item=[40], mean_pos=3.0,
+                           test_rows=20, name="wide_ns")
+    elif variant == "multi_nnz":
         ds = synth.general(seed=9, m=150, n=70, fu=3, fv=2, k=8, nnz_user=3, mean_pos=4.0, vals="real", test_rows=30)
     elif variant == "sparse":
         ds = synth.general(seed=13, m=120, n=90, fu=2, fv=2, k=4, d_user=[300, 7], d_item=[200, 5], mean_pos=0.7,
@@ -202,7 +214,7 @@ def test_variants_fp64(variant):
     for name, k in (("k1", 1), ("k5", 5), ("k16", 16), ("k64", 64), ("k100", 100)):
         if variant == name:
             kw["k"] = k
-    o, g = pair(ds, self_side=variant != "ns", freq=variant == "freq", **kw)
+    o, g = pair(ds, self_side=variant not in ("ns", "wide_ns"), freq=variant == "freq", **kw)
     # k >= 64: one epoch.  In the second, block (1,1)'s W half runs into the
     # 20-iteration CG cap (ffm.cpp:761) on this set, and that ill-conditioned
     # solve amplifies the reassociated sums (DPP trees vs the oracle's loops)

@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--precision", choices=["fp32", "fp64"], default="fp32")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-epochs", type=int, default=4)
+    ap.add_argument("--cpu-single-epochs", type=int, default=1, help="one-thread oracle epochs (0: skip)")
     ap.add_argument("--sgd", choices=["auto", "off"], default="auto",
                     help="N=1: also time the SGD/AdaGrad mode (tools/bench_sgd.py) into 'modes'")
     return ap.parse_args()
@@ -148,7 +149,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
-        cpu = cpu_baseline(ds, args.cpu_epochs)
+        cpu = cpu_baseline(ds, args.cpu_epochs, args.cpu_single_epochs)
     modes = None
     if world == 1 and args.sgd == "auto":
         modes = {"sgd": sgd_mode(ds, args)}
@@ -207,7 +208,7 @@ def sgd_mode(ds, args):
         return {"value": None, "error": str(e)}
 
 
-def cpu_baseline(ds, epochs):
+def cpu_baseline(ds, epochs, single_epochs=1):
     """The CPU oracle on a bounded sample: `epochs` epochs of the same
     kkbox-shaped problem, fp64, all host threads this process may use."""
     try:
@@ -217,9 +218,14 @@ def cpu_baseline(ds, epochs):
         ocffm.srand(1)
         o.init()
         secs = o.time_epochs(epochs, threads)
-        return {"value": round(ds.train.m * epochs / secs, 1), "unit": "instances/s", "cores": threads,
-                "kind": "port", "precision": "f64",
-                "sample": f"{epochs} epoch(s) of the same kkbox-shape problem ({ds.train.m} rows), {secs:.2f} s"}
+        out = {"value": round(ds.train.m * epochs / secs, 1), "unit": "instances/s", "cores": threads,
+               "kind": "port", "precision": "f64",
+               "sample": f"{epochs} epoch(s) of the same kkbox-shape problem ({ds.train.m} rows), {secs:.2f} s"}
+        if single_epochs > 0:  # also the one-thread rate (the reference's -c 1)
+            s1 = o.time_epochs(single_epochs, 1)
+            out["single_thread"] = {"value": round(ds.train.m * single_epochs / s1, 1), "cores": 1,
+                                    "sample": f"{single_epochs} epoch(s), {s1:.2f} s"}
+        return out
     except Exception as e:  # the baseline never blocks the GPU number
         return {"value": None, "unit": "instances/s", "cores": 0, "kind": "port", "sample": f"failed: {e}"}
 

@@ -843,6 +843,88 @@ __global__ __launch_bounds__(BLOCK) void k_hs_side_row(uint64_t R, const int64_t
   if (FUSE) fin_blocks<real, 1>(f, dsum);
 }
 
+// ------------------------------------------- per-column Grams (side) ---
+// A side half over a one-node-per-row field has, per feature column c,
+//   (X^T h)_c = sum_{i: idx_i = c} x_i h_i = G_c p_c,
+//   G_c = sum_{i: idx_i = c} d_i x_i^2 q1_i q1_i^T  (k x k, symmetric)
+// (hs_side row body, ffm.cpp:603-624, summed per column).  q1 and d are
+// fixed over the half's CG steps, so G_c is built once per half and each CG
+// step is one launch over D k^2 instead of a row pass plus a feature pass.
+// Rows per Gram chunk: the chunk's q1 rows are staged in 32 KB of LDS.
+// A chunk (one block) may span several such stages (host knob
+// OCFFM_CGRAM_CHUNK; measured at kkbox shape: 4 stages of 256 rows 110 us,
+// one stage of 256 rows 44 us, 128 rows 32 us (default), 64 rows 34 us).
+constexpr int cgram_rows(int kp, int rs) { return 32768 / (kp * rs) < 256 ? 32768 / (kp * rs) : 256; }
+
+// One block per chunk (Job: col, nparts = chunks of the column, [b, e) in
+// the field's CSC): each thread sums its entries of the chunk's rank-n
+// update; one-chunk columns store G_c, the chunks of longer columns add
+// into a zeroed G.
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_col_gram(const Job *__restrict__ chunks, const uint32_t *__restrict__ crow,
+                                                    const real *__restrict__ cval, const int64_t *__restrict__ yptr,
+                                                    const real *__restrict__ Q1, double w, double n1,
+                                                    real *__restrict__ G) {
+  constexpr int CH = cgram_rows(KP, (int)sizeof(real));
+  constexpr int NE = (KP * KP + BLOCK - 1) / BLOCK;
+  __shared__ real qs[CH * KP];
+  __shared__ real cs[CH];
+  const Job jb = chunks[blockIdx.x];
+  real acc[NE];
+#pragma unroll
+  for (int e = 0; e < NE; e++) acc[e] = 0;
+  for (int64_t b0 = jb.b; b0 < jb.e; b0 += CH) {  // LDS stages of CH rows
+    const int n = (int)(jb.e - b0 < CH ? jb.e - b0 : CH);
+    if (b0 != jb.b) __syncthreads();
+    for (int t = threadIdx.x; t < n * KP; t += BLOCK) qs[t] = Q1[(size_t)crow[b0 + t / KP] * KP + t % KP];
+    for (int r = threadIdx.x; r < n; r += BLOCK) {
+      const uint32_t i = crow[b0 + r];
+      const real x = cval[b0 + r];
+      cs[r] = (real)((1 - w) * (double)(yptr[i + 1] - yptr[i]) + w * n1) * x * x;
+    }
+    __syncthreads();
+    for (int r = 0; r < n; r++) {
+      const real c = cs[r];
+#pragma unroll
+      for (int e = 0; e < NE; e++) {
+        const int t = threadIdx.x + e * BLOCK;
+        if (t < KP * KP) acc[e] += c * qs[r * KP + t / KP] * qs[r * KP + t % KP];
+      }
+    }
+  }
+  real *g = G + (size_t)jb.col * KP * KP;
+#pragma unroll
+  for (int e = 0; e < NE; e++) {
+    const int t = threadIdx.x + e * BLOCK;
+    if (t < KP * KP) {
+      if (jb.nparts <= 1) g[t] = acc[e];
+      else unsafeAtomicAdd(g + t, acc[e]);
+    }
+  }
+}
+
+// One CG step of a Gram side half: per column, the direction p_c of
+// iteration f.it (formed from r, Hp, p as col_finalize does), s = G_c p_c,
+// then the Hessian-vector finalisation (MODE 1).  One column per subgroup.
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_hv_cgram(uint64_t D, const real *__restrict__ G, Fin<real> f) {
+  using Gm = Geo<real, KP>;
+  if (!f.st->run[f.it]) return;
+  const bool upd = f.it > 1;
+  const real alpha = upd ? (real)f.st->alpha : (real)0, beta = upd ? (real)f.st->beta : (real)0;
+  WAVE_SETUP
+  const int sg = lane / Gm::LPR, li = lane % Gm::LPR;
+  double dsum[3] = {0, 0, 0};
+  for (uint64_t c = wave * Gm::NSG + sg; c < D; c += nwaves * Gm::NSG) {
+    const FinOps<real> ops = fin_load<real, KP, 1>(f, (uint32_t)c, upd, li);
+    vec_t<real> pt = ops.w_or_p;
+    if (upd) pt = (ops.r - vsplat<real>(alpha) * ops.hp) + vsplat<real>(beta) * ops.w_or_p;
+    const vec_t<real> s = sg_vecmat<real, KP>(pt, G + c * KP * KP, li);
+    col_finalize<real, KP, 1>(f, (uint32_t)c, s, alpha, beta, upd, li, dsum, ops);
+  }
+  fin_blocks<real, 1>(f, dsum);
+}
+
 // Per segment of row i: h[s] = (1-w) sum_{j in seg} <phi_i, q_j> q_j
 // + [first] w phi_i QTQ, phi_i = X_i p  (hs_cross row body, ffm.cpp:715-738;
 // tau = X_i (V QTQ) = phi_i QTQ).  QTQ staged in LDS; phi_i's components

@@ -90,6 +90,10 @@ template <typename real> struct DevField {
   DevBuf<unsigned> cnt;  // per-column arrival tickets (zero at rest)
   bool idlike = false;   // one node per row and each feature in exactly one row (CSC = identity)
   bool one = false;      // exactly one node per row (xptr[i] == i)
+  // Per-column Grams (kernels.hpp k_col_gram / k_hv_cgram) of a one-node-per-row
+  // field with few columns: chunk jobs over the CSC and the D x k x k Grams.
+  DevBuf<Job> gchunks;
+  DevBuf<real> gram;
   // Owned field (several ranks): every feature is touched by the
   // rows of at most one rank.  Its CG vectors are then not all-reduced: each
   // rank finalises only the columns it owns (untouched ones go to rank 0) and
@@ -720,6 +724,7 @@ template <typename real> class Problem final : public ProblemBase {
       qtq_ = M_.p + (size_t)c0 * kp_ * kp_;
       heavy_grams(hc);
     }
+    col_grams(hc);
     // force iteration 1 to run
     CgState hs{};
     hs.run[1] = 1;
@@ -853,6 +858,9 @@ template <typename real> class Problem final : public ProblemBase {
       F->jobs.upload(jobs);
       F->njw = jobs.size() / nsg();
       F->cnt.alloc(std::max<uint64_t>(F->D, 1));
+      if (F->one && !F->idlike && cgram_on_ && R > 0 && F->D * kp_ <= 4 * R &&
+          F->D * kp_ * kp_ * sizeof(real) <= (1ull << 30))
+        col_gram_chunks(*F, xidx);
       F->h_xptr = std::move(xptr);
       F->h_xidx = std::move(xidx);
       F->h_xval = std::move(xval);
@@ -1377,6 +1385,44 @@ template <typename real> class Problem final : public ProblemBase {
     });
   }
 
+  // Gram chunks of a one-node-per-row field (build_csc's column order): each
+  // column in chunks of at most cgram_rows rows; empty columns get one empty
+  // chunk so that their G_c is stored as zero.
+  void col_gram_chunks(DevField<real> &F, const std::vector<uint32_t> &xidx) {
+    const uint64_t ch = std::min<uint64_t>(cgram_chunk_, (uint64_t)cgram_rows((int)kp_, (int)sizeof(real)));
+    std::vector<uint64_t> cptr(F.D + 1, 0);
+    for (uint32_t c : xidx) cptr[c + 1]++;
+    for (uint64_t d = 0; d < F.D; d++) cptr[d + 1] += cptr[d];
+    std::vector<Job> chunks;
+    for (uint64_t d = 0; d < F.D; d++) {
+      const uint64_t b = cptr[d], e = cptr[d + 1];
+      const uint32_t np = (uint32_t)std::max<uint64_t>(1, (e - b + ch - 1) / ch);
+      for (uint32_t q = 0; q < np; q++)
+        chunks.push_back(Job{(uint32_t)d, np, 0u, 0u, (int64_t)std::min(e, b + q * ch),
+                             (int64_t)std::min(e, b + (q + 1) * ch)});
+    }
+    F.gchunks.upload(chunks);
+    F.gram.alloc(F.D * kp_ * kp_, false);
+  }
+
+  // Side half whose CG steps run on per-column Grams (one GPU).
+  bool cgram(const HalfCtx &h) const { return !h.cross && h.F->gchunks.n && !comm_.active(); }
+
+  void col_grams(const HalfCtx &h) {
+    if (!cgram(h)) return;
+    DevField<real> &F = *h.F;
+    DevSide<real> &other = h.user ? V_ : U_;
+    HIPCHK(hipMemsetAsync(F.gram.p, 0, F.gram.bytes(), stream_));
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      const double rs = sizeof(real);
+      prof_launch("col_gram", (double)F.nnz * (8 + rs + 16 + KP * rs) + (double)F.gram.bytes(), [&] {
+        launch(k_col_gram<real, KP>, (unsigned)F.gchunks.n, BLOCK, 0, F.gchunks.p, F.crow.p, F.cval.p,
+               h.own->yptr.p, h.Q1, w_, (double)other.R, F.gram.p);
+      });
+    });
+  }
+
   // Row-complete cross half (kernels.hpp k_hs_cross_rc): fp32 at KP = 32,
   // one GPU, id-like field, and the heavy rows' Grams cheap to build (at most
   // a quarter of the side's positives in heavy rows: the items, whose heavy
@@ -1484,6 +1530,19 @@ template <typename real> class Problem final : public ProblemBase {
       }
       return;
     }
+    if (cgram(h)) {
+      with_kp(kp_, [&](auto K) {
+        constexpr int KP = decltype(K)::value;
+        using Gm = Geo<real, KP>;
+        const double rs = sizeof(real);
+        const Fin<real> fin = make_fin(h, it);
+        prof_launch("hv_cgram", (double)h.D * KP * KP * rs + (double)h.D * KP * rs * (it > 1 ? 9 : 4), [&] {
+          launch(k_hv_cgram<real, KP>, grid_for(h.D, 4 * Gm::NSG, 1024), BLOCK, 0, (uint64_t)h.D,
+                 (const real *)h.F->gram.p, fin);
+        });
+      });
+      return;
+    }
     const bool fz_ = fused_rows(h, true);
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
@@ -1544,6 +1603,7 @@ template <typename real> class Problem final : public ProblemBase {
     }
     gradient(h);
     heavy_grams(h);
+    col_grams(h);
     // CG with `lookahead_` iterations in flight (see file header): iteration
     // it is enqueued before the host waits for iteration it-L's verdict, so
     // the GPU never waits on the host.  Iterations past the real exit run as
@@ -1660,6 +1720,11 @@ template <typename real> class Problem final : public ProblemBase {
   // four gather rounds at the register budget of 3 waves/SIMD, where the
   // segment pass issues all 32 gathers at once at 4 waves/SIMD).
   bool rc_ = std::getenv("OCFFM_RC") != nullptr;
+  // OCFFM_CGRAM=0: side halves of small one-node-per-row fields take the row
+  // pass + feature pass instead of per-column Grams.
+  bool cgram_on_ = !std::getenv("OCFFM_CGRAM") || std::atoi(std::getenv("OCFFM_CGRAM")) != 0;
+  // OCFFM_CGRAM_CHUNK: rows per k_col_gram block (at most one LDS stage)
+  uint64_t cgram_chunk_ = std::getenv("OCFFM_CGRAM_CHUNK") ? std::max(1, std::atoi(std::getenv("OCFFM_CGRAM_CHUNK"))) : 128;
   // OCFFM_SCATTER=1: the cross update also writes the other orientation of
   // base by scattered 4-B stores instead of the gather kernel k_gather_pos
   // (measured 2 % slower per epoch: the scattered partial-line writes cost

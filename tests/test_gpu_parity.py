@@ -239,11 +239,15 @@ def test_kkbox_small_fp64(kk_small):
     np.testing.assert_allclose(vg["prec"], vo["prec"], atol=1e-12)
 
 
+@pytest.mark.parametrize("cgram", ["1", "0"])
 @pytest.mark.parametrize("precision", [ocffm.FP64, ocffm.FP32])
-def test_heavy_columns(precision):
+def test_heavy_columns(precision, cgram, monkeypatch):
     """Low-cardinality fields: columns with hundreds of rows go through the
     feature pass as several wave-chunks summed by the last to arrive
-    (kernels.hpp: Job), in both the row and the segment CSC."""
+    (kernels.hpp: Job), in both the row and the segment CSC.  With
+    OCFFM_CGRAM on (default) the side halves of the one-node fields run on
+    per-column Grams built from several chunks each (k_col_gram)."""
+    monkeypatch.setenv("OCFFM_CGRAM", cgram)
     ds = synth.general(seed=13, m=1500, n=300, fu=2, fv=2, k=8, d_user=[1500, 3], d_item=[300, 2], nnz_user=1,
                        mean_pos=12.0, vals="real")
     o, g = pair(ds, precision=precision, with_test=False)
@@ -265,7 +269,7 @@ def test_heavy_columns(precision):
 
 
 @pytest.mark.parametrize("env", [{"OCFFM_FUSE": "2"}, {"OCFFM_FUSE": "0"}, {"OCFFM_SEG_LEN": "3"}, {"OCFFM_LOOKAHEAD": "3"}, {"OCFFM_SCATTER": "1"},
-                                 {"OCFFM_FUSE": "2", "OCFFM_SEG_LEN": "2"}])
+                                 {"OCFFM_FUSE": "2", "OCFFM_SEG_LEN": "2"}, {"OCFFM_CGRAM": "0"}])
 def test_execution_variants_fp64(kk_small, monkeypatch, env):
     """Schedule knobs (id-field row fusion, segment length, CG look-ahead)
     change the kernels that run, never the result."""

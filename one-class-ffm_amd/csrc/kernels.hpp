@@ -507,6 +507,9 @@ __device__ __forceinline__ void col_finalize(const Fin<real> &f, uint32_t col, v
 // Grid-wide end of a finalising kernel.  MODE 0 publishes g2 and the first
 // CG verdict; MODE 1 computes alpha = r2/<p,Hp>, the new r2 (expanded),
 // beta and the verdict for iteration it+1 (ffm.cpp:780, 803-809).
+// The host copy of a verdict (run_host, host-mapped, polled by the host; it
+// clears the words before each half) is RUN_GO or RUN_STOP, never 0.
+constexpr int RUN_GO = 1, RUN_STOP = 2;
 template <typename real, int MODE>
 __device__ __forceinline__ void cg_publish(const Fin<real> &f, const double (&tot)[3]) {
   CgState *st = f.st;
@@ -514,13 +517,10 @@ __device__ __forceinline__ void cg_publish(const Fin<real> &f, const double (&to
     st->g2 = tot[0];
     st->r2 = tot[0];
     st->nr_cg = 0;
-    for (int i = 0; i <= MAXCG + 1; i++) {
-      st->run[i] = 0;
-      if (f.run_host) __hip_atomic_store(f.run_host + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    for (int i = 0; i <= MAXCG + 1; i++) st->run[i] = 0;
     const int go = (tot[0] * CG_EPS < tot[0]) ? 1 : 0;
     st->run[1] = go;
-    if (f.run_host) __hip_atomic_store(f.run_host + 1, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (f.run_host) __hip_atomic_store(f.run_host + 1, go ? RUN_GO : RUN_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   } else {
     const double r2 = st->r2;
     const double alpha = r2 / tot[0];
@@ -532,7 +532,8 @@ __device__ __forceinline__ void cg_publish(const Fin<real> &f, const double (&to
     st->nr_cg = f.it;
     const int go = (f.it < MAXCG && st->g2 * CG_EPS < r2n) ? 1 : 0;
     st->run[f.it + 1] = go;
-    if (f.run_host) __hip_atomic_store(f.run_host + f.it + 1, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (f.run_host)
+      __hip_atomic_store(f.run_host + f.it + 1, go ? RUN_GO : RUN_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -850,57 +851,107 @@ __global__ __launch_bounds__(BLOCK) void k_hs_side_row(uint64_t R, const int64_t
 // (hs_side row body, ffm.cpp:603-624, summed per column).  q1 and d are
 // fixed over the half's CG steps, so G_c is built once per half and each CG
 // step is one launch over D k^2 instead of a row pass plus a feature pass.
-// Rows per Gram chunk: the chunk's q1 rows are staged in 32 KB of LDS.
-// A chunk (one block) may span several such stages (host knob
-// OCFFM_CGRAM_CHUNK; measured at kkbox shape: 4 stages of 256 rows 110 us,
-// one stage of 256 rows 44 us, 128 rows 32 us (default), 64 rows 34 us).
+// Rows per Gram chunk: a chunk's q1 rows are staged once in 32 KB of LDS
+// (the host caps OCFFM_CGRAM_CHUNK at this).  Measured at kkbox shape:
+// 256-row chunks 44 us, 128 rows 32 us (default), 64 rows 34 us per build.
 constexpr int cgram_rows(int kp, int rs) { return 32768 / (kp * rs) < 256 ? 32768 / (kp * rs) : 256; }
 
-// One block per chunk (Job: col, nparts = chunks of the column, [b, e) in
-// the field's CSC): each thread sums its entries of the chunk's rank-n
-// update; one-chunk columns store G_c, the chunks of longer columns add
-// into a zeroed G.
+// One block per chunk (Job: col, nparts = chunks of the column, slot =
+// partial slot, flags = chunk index in the column, [b, e) in the field's
+// CSC, e - b <= cgram_rows): each thread sums its entries of the chunk's
+// rank-n update.  A one-chunk column stores G_c.  The chunks of a longer
+// column store their partials in consecutive slots (sc1), take a ticket on
+// the column, and the last to arrive sums the slots in chunk order:
+// deterministic, no float atomics (the guide's last-arriver hand-off: sc1
+// stores, every wave drained behind a barrier, one agent-scope add per
+// block, sc1 loads by the block whose add came last).
 template <typename real, int KP>
 __global__ __launch_bounds__(BLOCK) void k_col_gram(const Job *__restrict__ chunks, const uint32_t *__restrict__ crow,
                                                     const real *__restrict__ cval, const int64_t *__restrict__ yptr,
                                                     const real *__restrict__ Q1, double w, double n1,
-                                                    real *__restrict__ G) {
+                                                    real *__restrict__ G, real *__restrict__ gpart,
+                                                    unsigned *__restrict__ cnt) {
   constexpr int CH = cgram_rows(KP, (int)sizeof(real));
-  constexpr int NE = (KP * KP + BLOCK - 1) / BLOCK;
+  constexpr int KK = KP * KP;
+  constexpr int NE = (KK + BLOCK - 1) / BLOCK;
   __shared__ real qs[CH * KP];
   __shared__ real cs[CH];
+  __shared__ int s_last;
   const Job jb = chunks[blockIdx.x];
+  const int n = (int)(jb.e - jb.b);
+  for (int t = threadIdx.x; t < n * KP; t += BLOCK) qs[t] = Q1[(size_t)crow[jb.b + t / KP] * KP + t % KP];
+  for (int r = threadIdx.x; r < n; r += BLOCK) {
+    const uint32_t i = crow[jb.b + r];
+    const real x = cval[jb.b + r];
+    cs[r] = (real)((1 - w) * (double)(yptr[i + 1] - yptr[i]) + w * n1) * x * x;
+  }
+  __syncthreads();
   real acc[NE];
 #pragma unroll
   for (int e = 0; e < NE; e++) acc[e] = 0;
-  for (int64_t b0 = jb.b; b0 < jb.e; b0 += CH) {  // LDS stages of CH rows
-    const int n = (int)(jb.e - b0 < CH ? jb.e - b0 : CH);
-    if (b0 != jb.b) __syncthreads();
-    for (int t = threadIdx.x; t < n * KP; t += BLOCK) qs[t] = Q1[(size_t)crow[b0 + t / KP] * KP + t % KP];
-    for (int r = threadIdx.x; r < n; r += BLOCK) {
-      const uint32_t i = crow[b0 + r];
-      const real x = cval[b0 + r];
-      cs[r] = (real)((1 - w) * (double)(yptr[i + 1] - yptr[i]) + w * n1) * x * x;
-    }
-    __syncthreads();
-    for (int r = 0; r < n; r++) {
-      const real c = cs[r];
+  for (int r = 0; r < n; r++) {
+    const real c = cs[r];
 #pragma unroll
-      for (int e = 0; e < NE; e++) {
-        const int t = threadIdx.x + e * BLOCK;
-        if (t < KP * KP) acc[e] += c * qs[r * KP + t / KP] * qs[r * KP + t % KP];
-      }
+    for (int e = 0; e < NE; e++) {
+      const int t = threadIdx.x + e * BLOCK;
+      if (t < KK) acc[e] += c * qs[r * KP + t / KP] * qs[r * KP + t % KP];
     }
   }
-  real *g = G + (size_t)jb.col * KP * KP;
+  real *g = G + (size_t)jb.col * KK;
+  if (jb.nparts <= 1) {
+#pragma unroll
+    for (int e = 0; e < NE; e++) {
+      const int t = threadIdx.x + e * BLOCK;
+      if (t < KK) g[t] = acc[e];
+    }
+    return;
+  }
+  real *gp = gpart + (size_t)jb.slot * KK;
 #pragma unroll
   for (int e = 0; e < NE; e++) {
     const int t = threadIdx.x + e * BLOCK;
-    if (t < KP * KP) {
-      if (jb.nparts <= 1) g[t] = acc[e];
-      else unsafeAtomicAdd(g + t, acc[e]);
-    }
+    if (t < KK) __hip_atomic_store(gp + t, acc[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(cnt + jb.col, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == jb.nparts - 1;
+  __syncthreads();
+  if (!s_last) return;
+  // the column's slots, RB at a time per element (sc1 buffer loads: aux 16;
+  // slots past the column read zero), summed in slot order
+  constexpr int RB = NE >= 32 ? 1 : 32 / NE;
+  const BufView pv = buf_view(gpart + (size_t)(jb.slot - jb.flags) * KK, (uint64_t)jb.nparts * KK * sizeof(real));
+  real s[NE];
+#pragma unroll
+  for (int e = 0; e < NE; e++) s[e] = 0;
+  for (uint32_t q0 = 0; q0 < jb.nparts; q0 += RB) {
+    real y[NE][RB];
+#pragma unroll
+    for (int e = 0; e < NE; e++)
+#pragma unroll
+      for (int u = 0; u < RB; u++) {
+        const int t = threadIdx.x + e * BLOCK;
+        const uint32_t q = q0 + u;
+        const uint32_t off = (t < KK && q < jb.nparts) ? (uint32_t)((q * KK + t) * sizeof(real)) : pv.oob;
+        if constexpr (sizeof(real) == 4)
+          y[e][u] = __builtin_bit_cast(real, __builtin_amdgcn_raw_buffer_load_b32(pv.r, off, 0, 16));
+        else
+          y[e][u] = __builtin_bit_cast(real, __builtin_amdgcn_raw_buffer_load_b64(pv.r, off, 0, 16));
+      }
+#pragma unroll
+    for (int e = 0; e < NE; e++)
+#pragma unroll
+      for (int u = 0; u < RB; u++)
+        if (q0 + u == 0) s[e] = y[e][u];
+        else if (q0 + u < jb.nparts) s[e] += y[e][u];
+  }
+#pragma unroll
+  for (int e = 0; e < NE; e++) {
+    const int t = threadIdx.x + e * BLOCK;
+    if (t < KK) g[t] = s[e];
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(cnt + jb.col, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // One CG step of a Gram side half: per column, the direction p_c of
@@ -1323,6 +1374,17 @@ __global__ __launch_bounds__(BLOCK) void k_mask_rows(uint64_t nv, real *__restri
 }
 
 // ------------------------------------------------------- update rows ---
+// The CG step of an id-like field (each feature in exactly one row), with
+// the work of k_apply folded in by the row that owns the feature: the last
+// pending S += alpha p (ffm.cpp:806), then W += S (410, 441).  Returns S.
+template <typename real, int KP>
+__device__ __forceinline__ vec_t<real> apply_owned_row(const real *__restrict__ S, const real *__restrict__ Pd,
+                                                       real *__restrict__ W, real alpha, size_t off) {
+  const vec_t<real> s = vld<real>(S + off) + vsplat<real>(alpha) * vld<real>(Pd + off);
+  vst<real>(W + off, vld<real>(W + off) + s);
+  return s;
+}
+
 // Per segment of row i (one segment per subgroup): XS_i = X_i S;
 // [first] P_i += XS_i; base_ij += <XS_i, q_j> for the segment's positives
 // (update_cross, ffm.cpp:439-465), in this side's orientation; k_gather_pos
@@ -1339,17 +1401,24 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
                                                             uint64_t q1rows, const uint32_t *__restrict__ segd,
                                                             const real *__restrict__ segx,
                                                             real *__restrict__ yt_other,
-                                                            const uint32_t *__restrict__ perm) {
+                                                            const uint32_t *__restrict__ perm, real *__restrict__ W,
+                                                            const real *__restrict__ Pd, const CgState *st) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP>;
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real));
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
+  const real alpha = (W && st->nr_cg >= 1) ? (real)st->alpha : (real)0;
   for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) {
     const Seg sgm = segs[s];
     const uint64_t i = sgm.row;
     vec_t<real> xs = vzero<real>();
-    if (segd) {
+    if (W) {  // id-like field (segd set): the row's first segment does its feature's k_apply work
+      const size_t off = (size_t)segd[s] * KP + li * G::VE;
+      const vec_t<real> sf = seg_first(sgm) ? apply_owned_row<real, KP>(S, Pd, W, alpha, off)
+                                            : vld<real>(S + off) + vsplat<real>(alpha) * vld<real>(Pd + off);
+      xs = vsplat<real>(segx[s]) * sf;
+    } else if (segd) {
       xs = vsplat<real>(segx[s]) * vld<real>(S + (size_t)segd[s] * KP + li * G::VE);
     } else {
       for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
@@ -1424,19 +1493,28 @@ __global__ __launch_bounds__(BLOCK) void k_gather_pos(uint64_t n, const uint32_t
 // XS_i = X_i S; P_i += XS_i; a_i += <XS_i, q1_i>  (update_side,
 // ffm.cpp:405-437).  The reference also adds the gap to every positive of
 // row i; with y~ kept factored (see k_init_ytilde) that is implied by a_i.
-// One row per subgroup.
+// One row per subgroup.  W non-null (id-like field): the row also does its
+// feature's k_apply work (apply_owned_row).  The sum of the new a over the
+// side (b_sum of the next gd_side, ffm.cpp:551) goes to *asum, summed in a
+// fixed order (last_block).
 template <typename real, int KP>
 __global__ __launch_bounds__(BLOCK) void k_update_side_row(uint64_t R, const int64_t *__restrict__ xptr,
                                                            const uint32_t *__restrict__ xidx,
                                                            const real *__restrict__ xval, const real *__restrict__ S,
                                                            real *__restrict__ P1, const real *__restrict__ Q1,
-                                                           real *__restrict__ a1, bool one) {
+                                                           real *__restrict__ a1, bool one, real *__restrict__ W,
+                                                           const real *__restrict__ Pd, const CgState *st,
+                                                           double *__restrict__ asum, double *part, unsigned *tick) {
   using G = Geo<real, KP>;
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
+  const real alpha = (W && st->nr_cg >= 1) ? (real)st->alpha : (real)0;
+  double bs = 0;
   for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
     vec_t<real> xs = vzero<real>();
-    if (one) {
+    if (W) {  // id-like: one node per row, the row owns its feature
+      xs = vsplat<real>(xval[i]) * apply_owned_row<real, KP>(S, Pd, W, alpha, (size_t)xidx[i] * KP + li * G::VE);
+    } else if (one) {
       xs = vsplat<real>(xval[i]) * vld<real>(S + (size_t)xidx[i] * KP + li * G::VE);
     } else {
       for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
@@ -1444,8 +1522,15 @@ __global__ __launch_bounds__(BLOCK) void k_update_side_row(uint64_t R, const int
     }
     vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
     const real gap = sg_sum<G::LPR>(hsum<real>(xs * vld<real>(Q1 + i * KP + li * G::VE)));
-    if (li == 0) a1[i] += gap;
+    if (li == 0) {
+      const real an = a1[i] + gap;
+      a1[i] = an;
+      bs += (double)an;
+    }
   }
+  const double bv[1] = {block_sum(bs)};
+  double tot[1];
+  if (last_block<1>(bv, part, tick, tot) && threadIdx.x == 0) asum[0] = tot[0];
 }
 
 // ------------------------------------------------- partner aggregates ---

@@ -12,6 +12,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <charconv>
 #include <chrono>
 #include <cmath>
@@ -92,8 +93,11 @@ template <typename real> struct DevField {
   bool one = false;      // exactly one node per row (xptr[i] == i)
   // Per-column Grams (kernels.hpp k_col_gram / k_hv_cgram) of a one-node-per-row
   // field with few columns: chunk jobs over the CSC and the D x k x k Grams.
+  // Allocated on the first Gram half (col_grams); gpart holds the ordered
+  // partial slots of multi-chunk columns (gslots of them).
   DevBuf<Job> gchunks;
-  DevBuf<real> gram;
+  DevBuf<real> gram, gpart;
+  uint64_t gslots = 0;
   // Owned field (several ranks): every feature is touched by the
   // rows of at most one rank.  Its CG vectors are then not all-reduced: each
   // rank finalises only the columns it owns (untouched ones go to rank 0) and
@@ -373,6 +377,8 @@ template <typename real> class Problem final : public ProblemBase {
     h_.alloc(std::max<uint64_t>(std::max(Rmax, std::max(U_.nseg, V_.nseg)), 1) * kp_);
     if (std::max(U_.R, V_.R) * kp_ * sizeof(real) >= (1ull << 32) - 64)  // partner-row gathers (BufView)
       throw Error(OCFFM_E_DATA, "too many rows per GPU for 32-bit gather offsets; shard over more GPUs");
+    if (std::max(U_.npos, V_.npos) * 4 >= (1ull << 32) - 64)  // column reads through a BufView (k_hs_cross_w)
+      throw Error(OCFFM_E_DATA, "too many positives per GPU for 32-bit offsets; shard over more GPUs");
     if (h_.bytes() >= (1ull << 32) - 64)  // kernels.hpp: BufView gathers use 32-bit offsets
       throw Error(OCFFM_E_DATA, "too many rows/segments per GPU for one partial buffer; shard over more GPUs");
     uint64_t nslot = 1;
@@ -393,6 +399,7 @@ template <typename real> class Problem final : public ProblemBase {
     if (comm_.host_fn) HIPCHK(hipHostMalloc((void **)&stage_, Dmax * kp_ * sizeof(real), hipHostMallocDefault));
     if (comm_.host_fn) HIPCHK(hipHostMalloc((void **)&dstage_, DSTAGE * sizeof(double), hipHostMallocDefault));
     dots_.alloc(4);
+    bsum_.alloc(2);
   }
 
   ~Problem() override {
@@ -459,6 +466,7 @@ template <typename real> class Problem final : public ProblemBase {
     tmark("init: tables + UTX");
     cache_sasb();
     if (prm_.self_side) calc_side();
+    bias_sums();
     tmark("init: sasb + side");
     init_y_tilde();
     tmark("init: y~");
@@ -471,11 +479,31 @@ template <typename real> class Problem final : public ProblemBase {
   // OCFFM_TIMING=1: per epoch, host wall time and the part of it the host
   // spent blocked on the GPU (CG verdict waits).  Blocked most of the time =
   // GPU-bound; rarely blocked = the host's launch rate is the limit.
-  template <class F> void host_wait(F &&f) {
+  template <class F> auto host_wait(F &&f) {
     if (!timing_) return f();
     const auto t = std::chrono::steady_clock::now();
-    f();
+    auto r = f();
     wait_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    return r;
+  }
+  // Spin on the host-mapped verdict of CG iteration q until a finalising
+  // kernel has published it.  Every few thousand polls the stream is
+  // queried, so a faulted kernel surfaces as an error instead of a hang.
+  int poll_verdict(int q) {
+    for (uint64_t n = 1;; n++) {
+      const int v = __atomic_load_n(&run_host_[q], __ATOMIC_ACQUIRE);
+      if (v) return v;
+      if (n % 4096 == 0) {
+        const hipError_t e = hipStreamQuery(stream_);
+        if (e == hipSuccess) {  // stream drained: the word must be there now
+          const int w = __atomic_load_n(&run_host_[q], __ATOMIC_ACQUIRE);
+          if (w) return w;
+          throw Error(OCFFM_E_STATE, "CG verdict " + std::to_string(q) + " never published");
+        }
+        if (e != hipErrorNotReady) HIPCHK(e);
+      }
+      __builtin_ia32_pause();
+    }
   }
   bool timing_ = std::getenv("OCFFM_TIMING") != nullptr;
   double wait_ms_ = 0;
@@ -707,7 +735,9 @@ template <typename real> class Problem final : public ProblemBase {
   void grad(uint32_t f1, uint32_t f2, int half_id, double *out) override {
     need_init();
     HalfCtx hc = half_ctx(f1, f2, half_id);
+    want_g_ = true;
     gradient(hc);
+    want_g_ = false;
     copy_out(G_.p, hc.D, out);
   }
 
@@ -858,8 +888,8 @@ template <typename real> class Problem final : public ProblemBase {
       F->jobs.upload(jobs);
       F->njw = jobs.size() / nsg();
       F->cnt.alloc(std::max<uint64_t>(F->D, 1));
-      if (F->one && !F->idlike && cgram_on_ && R > 0 && F->D * kp_ <= 4 * R &&
-          F->D * kp_ * kp_ * sizeof(real) <= (1ull << 30))
+      if (F->one && !F->idlike && cgram_on_ && R > 0 && prm_.self_side && !comm_.active() &&
+          cgram_pays(R, F->D) && F->D * kp_ * kp_ * sizeof(real) <= (1ull << 30))
         col_gram_chunks(*F, xidx);
       F->h_xptr = std::move(xptr);
       F->h_xidx = std::move(xidx);
@@ -1077,6 +1107,16 @@ template <typename real> class Problem final : public ProblemBase {
       launch(k_rowdot_add<real, KP>, grid_for(R, 4 * Gm::NSG), BLOCK, 0, R, P, Q, acc);
       HIPCHK(hipGetLastError());
     });
+  }
+
+  // bsum_ = (sum of a over this rank's users, sum of b): the b_sum term of
+  // gd_side (ffm.cpp:551).  Kept current by k_update_side_row afterwards.
+  void bias_sums() {
+    for (int sd = 0; sd < 2; sd++) {
+      DevSide<real> &s = sd ? V_ : U_;
+      launch(k_vec_sum<real>, grid_for(s.R, BLOCK, 256), BLOCK, 0, (uint64_t)s.R, (const real *)s.bias.p,
+             bsum_.p + sd, part_.p, tick_.p);
+    }
   }
 
   // calc_side (ffm.cpp:360-373): a += <P,Q> over user-side blocks, b over item-side.
@@ -1314,11 +1354,7 @@ template <typename real> class Problem final : public ProblemBase {
         const uint32_t c0 = cross_slot(std::min(h.fl, h.fo), std::max(h.fl, h.fo));
         qtq_ = M_.p + (size_t)c0 * KP * KP;
       } else {
-        DevSide<real> &other = h.user ? V_ : U_;  // sum of the other side's bias (b_sum, ffm.cpp:551)
-        prof_launch("bias_sum", (double)other.R * rs, [&] {
-          launch(k_vec_sum<real>, grid_for(other.R, BLOCK, 256), BLOCK, 0, (uint64_t)other.R,
-                 (const real *)other.bias.p, sums_.p + 2 * KP, part_.p, tick_.p);
-        });
+        DevSide<real> &other = h.user ? V_ : U_;  // bsum_: sum of the other side's bias (b_sum, ffm.cpp:551)
         const double n1 = (double)other.R;
         const double bytes = (double)own.R * 8 + (double)own.npos * rs + (double)own.R * KP * rs * 2 +
                              (double)own.R * rs * 2;
@@ -1327,7 +1363,7 @@ template <typename real> class Problem final : public ProblemBase {
         auto go = [&](auto fz) {
           constexpr bool FZ = decltype(fz)::value;
           launch(k_gd_side_seg<real, KP, FZ>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, 0,
-              own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, own.bias.p, other.bias.p, own.s.p, sums_.p + 2 * KP,
+              own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, own.bias.p, other.bias.p, own.s.p, bsum_.p + (h.user ? 1 : 0),
               n1, w_, r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, (uint64_t)other.R, fin);
         };
         prof_launch(fz_ ? "gd_side_fused" : "gd_side_row", bytes, [&] {
@@ -1356,7 +1392,7 @@ template <typename real> class Problem final : public ProblemBase {
     f.fw = h.fw;
     f.lam = lam_;
     f.W = h.W1;
-    f.G = G_.p;
+    f.G = want_g_ ? G_.p : nullptr;
     f.S = S_.p;
     f.P = Vd_.p;
     f.R = Rv_.p;
@@ -1386,39 +1422,62 @@ template <typename real> class Problem final : public ProblemBase {
   }
 
   // Gram chunks of a one-node-per-row field (build_csc's column order): each
-  // column in chunks of at most cgram_rows rows; empty columns get one empty
-  // chunk so that their G_c is stored as zero.
+  // column in chunks of at most cgram_rows rows (one LDS stage: larger
+  // OCFFM_CGRAM_CHUNK values are capped there); empty columns get one empty
+  // chunk so that their G_c is stored as zero.  The chunks of a multi-chunk
+  // column get consecutive partial slots (Job.slot) and their index in the
+  // column (Job.flags).  The Gram buffers are allocated by col_grams.
   void col_gram_chunks(DevField<real> &F, const std::vector<uint32_t> &xidx) {
     const uint64_t ch = std::min<uint64_t>(cgram_chunk_, (uint64_t)cgram_rows((int)kp_, (int)sizeof(real)));
     std::vector<uint64_t> cptr(F.D + 1, 0);
     for (uint32_t c : xidx) cptr[c + 1]++;
     for (uint64_t d = 0; d < F.D; d++) cptr[d + 1] += cptr[d];
     std::vector<Job> chunks;
+    uint64_t slots = 0;
     for (uint64_t d = 0; d < F.D; d++) {
       const uint64_t b = cptr[d], e = cptr[d + 1];
       const uint32_t np = (uint32_t)std::max<uint64_t>(1, (e - b + ch - 1) / ch);
       for (uint32_t q = 0; q < np; q++)
-        chunks.push_back(Job{(uint32_t)d, np, 0u, 0u, (int64_t)std::min(e, b + q * ch),
-                             (int64_t)std::min(e, b + (q + 1) * ch)});
+        chunks.push_back(Job{(uint32_t)d, np, np > 1 ? (uint32_t)(slots + q) : 0u, q,
+                             (int64_t)std::min(e, b + q * ch), (int64_t)std::min(e, b + (q + 1) * ch)});
+      if (np > 1) slots += np;
     }
+    if (slots > 0xffffffffull) throw Error(OCFFM_E_DATA, "too many Gram chunks in one field");
     F.gchunks.upload(chunks);
-    F.gram.alloc(F.D * kp_ * kp_, false);
+    F.gslots = slots;
   }
 
   // Side half whose CG steps run on per-column Grams (one GPU).
   bool cgram(const HalfCtx &h) const { return !h.cross && h.F->gchunks.n && !comm_.active(); }
 
+  // Does a side half over a one-node-per-row field (R rows, D columns) pay
+  // for its Grams?  Estimated time (us) of a half of `c` CG steps, from the
+  // kkbox-shape measurements: ~4 TB/s effective for the
+  // streamed bytes, ~4.1e6 rank-1 MACs per us for the build, dispatch
+  // floors of 5 us (one launch) and 10 us (row pass + feature pass).
+  //   Gram: build + c (D k^2 + 9 D k) s     rows: c (4 R k + 9 D k) s
+  // OCFFM_CGRAM=2 takes the Gram path wherever the structure allows.
+  bool cgram_pays(uint64_t R, uint64_t D) const {
+    if (cgram_mode_ == 2) return true;
+    const double k = (double)kp_, s = sizeof(real), bw = 4e6, c = 4;
+    const double build = 5 + (double)R * k * k / 4.1e6 + ((double)R * k + (double)D * k * k) * s / bw;
+    const double gstep = 5 + ((double)D * k * k + 9.0 * D * k) * s / bw;
+    const double rstep = 10 + (4.0 * R * k + 9.0 * D * k) * s / bw;
+    return build + c * gstep <= c * rstep;
+  }
+
   void col_grams(const HalfCtx &h) {
     if (!cgram(h)) return;
     DevField<real> &F = *h.F;
     DevSide<real> &other = h.user ? V_ : U_;
-    HIPCHK(hipMemsetAsync(F.gram.p, 0, F.gram.bytes(), stream_));
+    if (!F.gram.p) F.gram.alloc(F.D * kp_ * kp_, false);  // every column is stored by its last chunk
+    if (F.gslots && !F.gpart.p) F.gpart.alloc(F.gslots * kp_ * kp_, false);
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
       const double rs = sizeof(real);
       prof_launch("col_gram", (double)F.nnz * (8 + rs + 16 + KP * rs) + (double)F.gram.bytes(), [&] {
         launch(k_col_gram<real, KP>, (unsigned)F.gchunks.n, BLOCK, 0, F.gchunks.p, F.crow.p, F.cval.p,
-               h.own->yptr.p, h.Q1, w_, (double)other.R, F.gram.p);
+               h.own->yptr.p, h.Q1, w_, (double)other.R, F.gram.p, F.gpart.p, F.cnt.p);
       });
     });
   }
@@ -1601,6 +1660,12 @@ template <typename real> class Problem final : public ProblemBase {
       hb = ev();
       HIPCHK(hipEventRecord(hb, stream_));
     }
+    // The verdicts of this half start unknown (0); the finalising kernels
+    // publish RUN_GO / RUN_STOP into the host-mapped words (kernels.hpp
+    // cg_publish).  Nothing of the previous half can still write them: its
+    // last verdict has been read and the iterations queued past it are no-ops.
+    std::memset(run_host_, 0, sizeof(int) * (MAXCG + 2));
+    std::atomic_thread_fence(std::memory_order_seq_cst);
     gradient(h);
     heavy_grams(h);
     col_grams(h);
@@ -1608,32 +1673,25 @@ template <typename real> class Problem final : public ProblemBase {
     // it is enqueued before the host waits for iteration it-L's verdict, so
     // the GPU never waits on the host.  Iterations past the real exit run as
     // no-ops.  The count of iterations that ran is the last t with run[t].
-    std::vector<hipEvent_t> evs;
+    // The host polls the verdict words instead of synchronising on events:
+    // an event recorded between two CG steps cost ~5 us of GPU idle per step
+    // (measured: 6.7 us vs 1.1 us at the boundaries without one).
     int nr = 0, known = 0;
     bool done = false;
     auto examine = [&](int upto) {
       for (int q = known + 1; q <= upto && q <= MAXCG && !done; q++) {
-        if (!__atomic_load_n(&run_host_[q], __ATOMIC_ACQUIRE)) done = true;
+        const int v = host_wait([&] { return poll_verdict(q); });
+        if (v != RUN_GO) done = true;
         else nr = q;
         known = q;
       }
     };
     for (int it = 1; it <= MAXCG && !done; it++) {
       hv_pass(h, it);
-      hipEvent_t e = ev();
-      HIPCHK(hipEventRecord(e, stream_));
-      evs.push_back(e);
       const int t = it - lookahead_;
-      if (t >= 1) {
-        host_wait([&] { HIPCHK(hipEventSynchronize(evs[t - 1])); });
-        examine(t + 1);  // upd(t) decided run[t+1]
-      }
+      if (t >= 1) examine(t + 1);  // upd(t) decided run[t+1]
     }
-    if (!done) {
-      host_wait([&] { HIPCHK(hipEventSynchronize(evs.back())); });
-      examine(MAXCG);
-    }
-    for (auto e : evs) ev_free_.push_back(e);
+    if (!done) examine(MAXCG);
     // apply + update
     DevSide<real> &own = *h.own;
     with_kp(kp_, [&](auto K) {
@@ -1643,12 +1701,17 @@ template <typename real> class Problem final : public ProblemBase {
       const uint64_t nv = h.D * KP / Gm::VE;
       const bool excl = h.F->excl;
       if (excl) owned_stale_ = true;
-      prof_launch("apply_step", (double)h.D * KP * rs * 5, [&] {
-        launch(k_apply<real>, grid_for(nv, BLOCK, 2048), BLOCK, 0, nv, Vd_.p, S_.p, h.W1, st_.p,
-               excl ? (const uint8_t *)h.F->own.p : nullptr, (uint32_t)Gm::LPR);
-      });
-      if (own.R == 0) return;
+      // id-like field: each feature's row does its k_apply work in the update
+      // kernel (apply_owned_row), one launch fewer at the end of the half
       DevField<real> &F = *h.F;
+      const bool fold = F.idlike && own.R > 0 && !excl && !no_fold_;
+      real *Wf = fold ? h.W1 : nullptr;
+      if (!fold)
+        prof_launch("apply_step", (double)h.D * KP * rs * 5, [&] {
+          launch(k_apply<real>, grid_for(nv, BLOCK, 2048), BLOCK, 0, nv, Vd_.p, S_.p, h.W1, st_.p,
+                 excl ? (const uint8_t *)h.F->own.p : nullptr, (uint32_t)Gm::LPR);
+        });
+      if (own.R == 0) return;
       if (h.cross) {
         DevSide<real> &other = *h.partner;
         const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
@@ -1657,7 +1720,8 @@ template <typename real> class Problem final : public ProblemBase {
         prof_launch("update_cross_row", bytes, [&] {
           launch(k_update_cross_seg<real, KP>, grid_for(own.nseg, 4 * Gm::NSG), BLOCK, 0,
               own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, own.ycol.p, own.yt.p, h.Q1,
-              (uint64_t)other.R, F.segd.p, F.segx.p, scatter_ ? other.yt.p : nullptr, own.perm.p);
+              (uint64_t)other.R, F.segd.p, F.segx.p, scatter_ ? other.yt.p : nullptr, own.perm.p, Wf,
+              (const real *)Vd_.p, (const CgState *)st_.p);
         });
         if (!scatter_) refresh_other(own, other);  // gather the other orientation instead
       } else {
@@ -1666,7 +1730,8 @@ template <typename real> class Problem final : public ProblemBase {
                              (double)own.R * KP * rs * 3 + (double)own.R * rs * 2 + (double)own.npos * (4 + 4 * rs);
         prof_launch("update_side_row", bytes, [&] {
           launch(k_update_side_row<real, KP>, grid_for(own.R, 4 * Gm::NSG), BLOCK, 0,
-              own.R, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, h.Q1, own.bias.p, F.one);
+              own.R, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, h.Q1, own.bias.p, F.one, Wf,
+              (const real *)Vd_.p, (const CgState *)st_.p, bsum_.p + (h.user ? 0 : 1), part_.p, tick_.p);
         });
       }
     });
@@ -1720,10 +1785,15 @@ template <typename real> class Problem final : public ProblemBase {
   // four gather rounds at the register budget of 3 waves/SIMD, where the
   // segment pass issues all 32 gathers at once at 4 waves/SIMD).
   bool rc_ = std::getenv("OCFFM_RC") != nullptr;
-  // OCFFM_CGRAM=0: side halves of small one-node-per-row fields take the row
-  // pass + feature pass instead of per-column Grams.
-  bool cgram_on_ = !std::getenv("OCFFM_CGRAM") || std::atoi(std::getenv("OCFFM_CGRAM")) != 0;
-  // OCFFM_CGRAM_CHUNK: rows per k_col_gram block (at most one LDS stage)
+  // OCFFM_NO_FOLD=1: k_apply as its own launch on id-like fields too
+  bool no_fold_ = std::getenv("OCFFM_NO_FOLD") != nullptr;
+  // OCFFM_CGRAM: side halves of one-node-per-row fields run their CG steps
+  // on per-column Grams where cgram_pays() (1, default), never (0), or
+  // wherever the structure allows (2).
+  int cgram_mode_ = std::getenv("OCFFM_CGRAM") ? std::atoi(std::getenv("OCFFM_CGRAM")) : 1;
+  bool cgram_on_ = cgram_mode_ != 0;
+  // OCFFM_CGRAM_CHUNK: rows per k_col_gram block, capped at one LDS stage
+  // (cgram_rows: 256 rows at k = 32 fp32)
   uint64_t cgram_chunk_ = std::getenv("OCFFM_CGRAM_CHUNK") ? std::max(1, std::atoi(std::getenv("OCFFM_CGRAM_CHUNK"))) : 128;
   // OCFFM_SCATTER=1: the cross update also writes the other orientation of
   // base by scattered 4-B stores instead of the gather kernel k_gather_pos
@@ -1742,6 +1812,8 @@ template <typename real> class Problem final : public ProblemBase {
   std::vector<Block> blocks_;
   std::vector<DevBuf<real>> W_, H_, P_, Q_;
   DevBuf<real> acc_, G_, S_, Vd_, Rv_, Hv_, h_, M_, wpart_;
+  DevBuf<double> bsum_;  // sums of a and b (bias_sums)
+  bool want_g_ = false;  // grad(): the gradient finalisation also stores G
   const real *qtq_ = nullptr;  // this cross half's Q^T Q: a slot of M_
   DevBuf<unsigned> tick_;
   DevBuf<double> sums_, vecs_, part_, at_d_, popular_;

@@ -239,17 +239,20 @@ def test_kkbox_small_fp64(kk_small):
     np.testing.assert_allclose(vg["prec"], vo["prec"], atol=1e-12)
 
 
-@pytest.mark.parametrize("cgram", ["1", "0"])
+HEAVY = dict(seed=13, m=1500, n=300, fu=2, fv=2, k=8, d_user=[1500, 3], d_item=[300, 2], nnz_user=1,
+             mean_pos=12.0, vals="real")
+
+
+@pytest.mark.parametrize("cgram", ["2", "0"])
 @pytest.mark.parametrize("precision", [ocffm.FP64, ocffm.FP32])
 def test_heavy_columns(precision, cgram, monkeypatch):
     """Low-cardinality fields: columns with hundreds of rows go through the
     feature pass as several wave-chunks summed by the last to arrive
     (kernels.hpp: Job), in both the row and the segment CSC.  With
-    OCFFM_CGRAM on (default) the side halves of the one-node fields run on
-    per-column Grams built from several chunks each (k_col_gram)."""
+    OCFFM_CGRAM=2 the side halves of the one-node fields run on per-column
+    Grams built from several chunks each (k_col_gram: ordered partial slots)."""
     monkeypatch.setenv("OCFFM_CGRAM", cgram)
-    ds = synth.general(seed=13, m=1500, n=300, fu=2, fv=2, k=8, d_user=[1500, 3], d_item=[300, 2], nnz_user=1,
-                       mean_pos=12.0, vals="real")
+    ds = synth.general(**HEAVY)
     o, g = pair(ds, precision=precision, with_test=False)
     for _ in range(2):
         o.one_epoch()
@@ -268,8 +271,35 @@ def test_heavy_columns(precision, cgram, monkeypatch):
         assert abs(gpu_objective(o2, g) - f_ref) <= 1e-3 * abs(f_ref)
 
 
+@pytest.mark.parametrize("ds_name", ["heavy", "kkbox_s"])
+def test_fp32_runs_bit_identical(ds_name, monkeypatch):
+    """The default fp32 path has no order-dependent float sums (feature
+    passes, Gram builds and grid reductions combine in a fixed order): two
+    runs of the same epochs give bit-identical tables and CG logs.  "heavy"
+    forces the Gram path onto multi-chunk columns (k_col_gram's partial slots)."""
+    if ds_name == "heavy":
+        monkeypatch.setenv("OCFFM_CGRAM", "2")
+        ds = synth.general(**HEAVY)
+    else:
+        ds = synth.kkbox(m=3000, n=4000, mean=20.0, seed=11, name="kk_det")
+    runs = []
+    for _ in range(2):
+        g = ocffm.problem_from_dataset(ds, precision=ocffm.FP32, with_test=False)
+        ocffm.srand(1)
+        g.init()
+        for _ in range(2):
+            g.one_epoch()
+        o = O.Oracle(ds, with_test=False)  # only for the block list
+        runs.append(([g.get(w, b) for b in state_names(o) for w in "WH"], g.cg_log().copy()))
+        g.close()
+    for a, b in zip(runs[0][0], runs[1][0]):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(runs[0][1], runs[1][1])
+
+
 @pytest.mark.parametrize("env", [{"OCFFM_FUSE": "2"}, {"OCFFM_FUSE": "0"}, {"OCFFM_SEG_LEN": "3"}, {"OCFFM_LOOKAHEAD": "3"}, {"OCFFM_SCATTER": "1"},
-                                 {"OCFFM_FUSE": "2", "OCFFM_SEG_LEN": "2"}, {"OCFFM_CGRAM": "0"}])
+                                 {"OCFFM_FUSE": "2", "OCFFM_SEG_LEN": "2"}, {"OCFFM_CGRAM": "0"},
+                                 {"OCFFM_NO_FOLD": "1"}])
 def test_execution_variants_fp64(kk_small, monkeypatch, env):
     """Schedule knobs (id-field row fusion, segment length, CG look-ahead)
     change the kernels that run, never the result."""

@@ -412,6 +412,10 @@ template <typename real> struct Fin {
   double *dots;    // non-null: the grid's dot products are this rank's partials;
                    // the last block stores them here for a cross-rank sum and
                    // k_cg_step publishes the CG scalars (owned fields)
+  // column tau (k_feat<..., TAU>): the w phi_i QTQ term of hs_cross for a
+  // one-node-per-row field, summed per column: w (sum_{i in col} x_i^2) p QTQ
+  const real *xsq;  // per column: sum of x^2 over its rows
+  double tw;        // w
 };
 
 // A column receiving `nparts` partial sums: each part adds into acc and takes
@@ -466,9 +470,10 @@ __device__ __forceinline__ FinOps<real> fin_load(const Fin<real> &f, uint32_t co
   }
   return o;
 }
-template <typename real, int KP, int MODE>
+template <typename real, int KP, int MODE, bool TAU = false>
 __device__ __forceinline__ void col_finalize(const Fin<real> &f, uint32_t col, vec_t<real> s, real alpha, real beta,
-                                             bool upd, int li, double (&ds)[3], const FinOps<real> &o) {
+                                             bool upd, int li, double (&ds)[3], const FinOps<real> &o,
+                                             const real *tq = nullptr) {
   using G = Geo<real, KP>;
   const size_t off = (size_t)col * KP + li * G::VE;
   if (MODE == 0) {
@@ -488,6 +493,7 @@ __device__ __forceinline__ void col_finalize(const Fin<real> &f, uint32_t col, v
       vst<real>(f.R + off, rn);
       vst<real>(f.P + off, pe);
     }
+    if constexpr (TAU) s += vsplat<real>((real)(f.tw * (double)f.xsq[col])) * sg_vecmat<real, KP>(pe, tq, li);
     const vec_t<real> hp = vsplat<real>(o.reg) * pe + s;
     vst<real>(f.Hp + off, hp);
 #pragma unroll
@@ -1001,8 +1007,9 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
   extern __shared__ __align__(16) unsigned char smem_raw[];
   real *Qs = reinterpret_cast<real *>(smem_raw);
   const real *Qp = QTQ;
-  if (MLDS) {
-    for (int t = threadIdx.x; t < KP * KP; t += BLOCK) Qs[t] = QTQ[t];
+  if (MLDS) {  // QTQ null: the tau term is added per column by the feature pass (k_feat TAU)
+    if (QTQ)
+      for (int t = threadIdx.x; t < KP * KP; t += BLOCK) Qs[t] = QTQ[t];
     __syncthreads();
     Qp = Qs;
   }
@@ -1064,7 +1071,7 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
       });
     }
     vec_t<real> out = vsplat<real>(cpos) * ka;
-    if (seg_first(sgm)) {
+    if (QTQ && seg_first(sgm)) {
       out += vsplat<real>((real)w) * sg_vecmat<real, KP>(phi, Qp, li);
     }
     if (!FUSE) {
@@ -1239,13 +1246,20 @@ __global__ __launch_bounds__(BLOCK) void k_hs_cross_rc(uint64_t R, const int64_t
 // MODE 0: gradient finalisation, MODE 1: Hessian-vector finalisation of CG
 // iteration f.it (col_finalize above), MODE 2: store the column sums into
 // f.acc (multi-GPU: the all-reduce and k_fin follow).
-template <typename real, int KP, int MODE, int JE = JOB_ENT>
+template <typename real, int KP, int MODE, int JE = JOB_ENT, bool TAU = false>
 __global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__restrict__ jobs,
                                                 const uint32_t *__restrict__ crow, const real *__restrict__ cval,
                                                 const real *__restrict__ h, uint64_t hbytes, real *__restrict__ wpart,
-                                                Fin<real> f) {
+                                                Fin<real> f, const real *__restrict__ QTQ) {
   using G = Geo<real, KP>;
   if (f.it > 0 && !f.st->run[f.it]) return;
+  // TAU (MODE 1): QTQ staged in LDS for the per-column tau term
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  real *Qs = reinterpret_cast<real *>(smem_raw);
+  if constexpr (TAU) {
+    for (int t = threadIdx.x; t < KP * KP; t += BLOCK) Qs[t] = QTQ[t];
+    __syncthreads();
+  }
   const BufView hb = buf_view(h, hbytes);
   const bool upd = MODE == 1 && f.it > 1;
   const real alpha = upd ? (real)f.st->alpha : (real)0, beta = upd ? (real)f.st->beta : (real)0;
@@ -1317,7 +1331,7 @@ __global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__res
     }
     if (mine) {
       if (MODE == 2) vst<real>(f.acc + (size_t)jb.col * KP + li * G::VE, s);
-      else col_finalize<real, KP, (MODE == 2 ? 0 : MODE)>(f, jb.col, s, alpha, beta, upd, li, dsum, ops);
+      else col_finalize<real, KP, (MODE == 2 ? 0 : MODE), TAU>(f, jb.col, s, alpha, beta, upd, li, dsum, ops, Qs);
     }
   }
   if (MODE != 2) fin_blocks<real, (MODE == 2 ? 0 : MODE)>(f, dsum);

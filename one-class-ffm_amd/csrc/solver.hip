@@ -83,6 +83,7 @@ template <typename real> struct DevField {
   DevBuf<Job> jobs;  // kernels.hpp: Job; njw waves of NSG jobs
   uint64_t njw = 0, nslot = 0;
   DevBuf<real> freqw;  // global feature frequency (for --freq)
+  DevBuf<real> xsq;    // one node per row: sum of x^2 over each column's rows (column tau)
   // the same CSC over positive segments (kernels.hpp: Seg) of the side
   DevBuf<uint32_t> scrow;
   DevBuf<real> scval;
@@ -878,6 +879,11 @@ template <typename real> class Problem final : public ProblemBase {
       F->xptr.upload(xptr);
       F->xidx.upload(xidx);
       F->xval.upload(to_real(xval));
+      if (F->one) {
+        std::vector<double> sq(std::max<uint64_t>(F->D, 1), 0.0);
+        for (uint64_t i = 0; i < R; i++) sq[xidx[i]] += xval[i] * xval[i];
+        F->xsq.upload(to_real(sq));
+      }
       std::vector<uint32_t> crow;
       std::vector<double> cval;
       std::vector<Job> jobs;
@@ -1405,6 +1411,8 @@ template <typename real> class Problem final : public ProblemBase {
     f.run_host = run_host_dev_;
     f.it = it;
     f.dots = h.F->excl ? dots_.p : nullptr;
+    f.xsq = nullptr;
+    f.tw = w_;
     return f;
   }
   // id-like field on one GPU: the row pass finalises its feature column.
@@ -1491,6 +1499,18 @@ template <typename real> class Problem final : public ProblemBase {
            h.own->heavy_pos * 4 <= h.own->npos;
   }
 
+  // Column tau: the w phi_i QTQ term of a cross half's Hessian-vector rows,
+  // for a one-node-per-row field, is w (sum_{i in col d} x_i^2) p_d QTQ per
+  // column, added by the feature pass (k_feat TAU) instead of per row by
+  // k_hs_cross_seg: one k x k product per column instead of per row (items
+  // over artist / genre: 100,000 rows, 5,000 / 50 columns).  One GPU (on
+  // several ranks the item halves' QTQ is a partial over local users).
+  static constexpr size_t COLTAU_LDS = 32 * 1024;
+  bool coltau(const HalfCtx &h) const {
+    return coltau_on_ && h.cross && h.F->one && !comm_.active() && !fused_rows(h, true) && !row_complete(h) &&
+           (size_t)kp_ * kp_ * sizeof(real) <= COLTAU_LDS;
+  }
+
   // fuse_ 1: the Hessian-vector pass of side halves only (one row = one
   // feature, no partial sums); 2: every row pass (the gradient passes and the
   // cross halves walk positive segments, whose multi-segment rows meet through
@@ -1521,15 +1541,28 @@ template <typename real> class Problem final : public ProblemBase {
       const double bytes = (double)ent * (4 + rs) + (double)ent * KP * rs + (double)njw * Gm::NSG * sizeof(Job) +
                            (double)h.D * KP * rs * vecs;
       const unsigned grid = (unsigned)std::min<uint64_t>((njw + 3) / 4, feat_blocks_);  // grid-stride: fewer tickets
-      const Fin<real> fin = make_fin(h, it);
+      Fin<real> fin = make_fin(h, it);
       const Job *jobs = seg ? F.sjobs.p : F.jobs.p;
       const uint32_t *crow = seg ? F.scrow.p : F.crow.p;
       const real *cval = seg ? F.scval.p : F.cval.p;
       const char *name = mode == 2 ? "csc_scatter" : (mode == 0 ? "feat_grad" : "feat_hv");
+      const real *nq = nullptr;
       prof_launch(name, bytes, [&] {
-        if (mode == 0) launch(k_feat<real, KP, 0>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, fin);
-        else if (mode == 1) launch(k_feat<real, KP, 1>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, fin);
-        else launch(k_feat<real, KP, 2>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, fin);
+        if (mode == 0) {
+          launch(k_feat<real, KP, 0>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, fin, nq);
+        } else if (mode == 1) {
+          if constexpr ((size_t)KP * KP * sizeof(real) <= COLTAU_LDS) {
+            if (coltau(h)) {
+              fin.xsq = F.xsq.p;
+              launch(k_feat<real, KP, 1, JOB_ENT, true>, grid, BLOCK, (size_t)KP * KP * sizeof(real), njw, jobs, crow,
+                     cval, h_.p, h_.bytes(), wpart_.p, fin, (const real *)qtq_);
+              return;
+            }
+          }
+          launch(k_feat<real, KP, 1>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, fin, nq);
+        } else {
+          launch(k_feat<real, KP, 2>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, fin, nq);
+        }
       });
     });
   }
@@ -1619,7 +1652,7 @@ template <typename real> class Problem final : public ProblemBase {
           auto go = [&](auto fz, auto ml) {
             constexpr bool FZ = decltype(fz)::value, ML = decltype(ml)::value;
             launch(k_hs_cross_seg<real, KP, ML, FZ>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : hs_blocks_), BLOCK, smem, own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p,
-                                                         own.ycol.p, h.Q1, (uint64_t)h.partner->R, qtq_, w_, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
+                                                         own.ycol.p, h.Q1, (uint64_t)h.partner->R, coltau(h) ? (const real *)nullptr : (const real *)qtq_, w_, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
                                                          F.segd.p, F.segx.p, fin);
           };
           prof_launch(fz_ ? "hs_cross_fused" : "hs_cross_row", bytes, [&] {
@@ -1785,6 +1818,8 @@ template <typename real> class Problem final : public ProblemBase {
   // four gather rounds at the register budget of 3 waves/SIMD, where the
   // segment pass issues all 32 gathers at once at 4 waves/SIMD).
   bool rc_ = std::getenv("OCFFM_RC") != nullptr;
+  // OCFFM_COLTAU=0: the tau term of cross Hessian-vector rows per row (k_hs_cross_seg)
+  bool coltau_on_ = !std::getenv("OCFFM_COLTAU") || std::atoi(std::getenv("OCFFM_COLTAU")) != 0;
   // OCFFM_NO_FOLD=1: k_apply as its own launch on id-like fields too
   bool no_fold_ = std::getenv("OCFFM_NO_FOLD") != nullptr;
   // OCFFM_CGRAM: side halves of one-node-per-row fields run their CG steps

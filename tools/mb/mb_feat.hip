@@ -104,7 +104,7 @@ int main(int argc, char **argv) {
   {
     float us1 = 0;
     for (unsigned g : {512u, 1024u, 2048u, (unsigned)((njw + 3) / 4)}) {
-      us1 = timeit([&] { k_feat<float, KP, 1, 1><<<std::min(g, (unsigned)((njw + 3) / 4)), 256>>>(njw, jobs, crow, cval, h, D * KP * 4, wpart, Fin<float>{nullptr, 1.0, W, nullptr, S, P, R, Hp, acc, cnt, st, part, tick_, nullptr, 2}); }, 50);
+      us1 = timeit([&] { k_feat<float, KP, 1, 1><<<std::min(g, (unsigned)((njw + 3) / 4)), 256>>>(njw, jobs, crow, cval, h, D * KP * 4, wpart, Fin<float>{nullptr, 1.0, W, nullptr, S, P, R, Hp, acc, cnt, st, part, tick_, nullptr, 2}, nullptr); }, 50);
       std::printf("k_feat JE=1 MODE1 grid %u: %8.2f us\n", g, us1);
     }
   }

@@ -418,29 +418,6 @@ template <typename real> struct Fin {
   double tw;        // w
 };
 
-// A column receiving `nparts` partial sums: each part adds into acc and takes
-// a ticket; the last to arrive gets the total back (atomic exchange also
-// re-zeroes acc) and finalises.  One-part columns finalise directly.
-template <typename real, int KP>
-__device__ __forceinline__ bool col_arrive(const Fin<real> &f, uint32_t col, unsigned nparts, vec_t<real> &s, int sg,
-                                           int li) {
-  using G = Geo<real, KP>;
-  if (nparts <= 1) return true;
-  const size_t off = (size_t)col * KP + li * G::VE;
-#pragma unroll
-  for (int e = 0; e < G::VE; e++) unsafeAtomicAdd(f.acc + off + e, s[e]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  unsigned t = 0;
-  if (li == 0) t = __hip_atomic_fetch_add(f.cnt + col, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  t = __shfl(t, sg * G::LPR, 64);
-  if (t != nparts - 1) return false;
-#pragma unroll
-  for (int e = 0; e < G::VE; e++)
-    s[e] = __hip_atomic_exchange(f.acc + off + e, (real)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (li == 0) __hip_atomic_store(f.cnt + col, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return true;
-}
-
 // MODE 0 (gradient, ffm.cpp:561-570, 773-779): G = lam f W + s; r = -G;
 //   p = r; S = 0; ds[0] += |G|^2.
 // MODE 1 (Hessian-vector, ffm.cpp:783-809): apply iteration it-1's update
@@ -508,6 +485,93 @@ template <typename real, int KP, int MODE>
 __device__ __forceinline__ void col_finalize(const Fin<real> &f, uint32_t col, vec_t<real> s, real alpha, real beta,
                                              bool upd, int li, double (&ds)[3]) {
   col_finalize<real, KP, MODE>(f, col, s, alpha, beta, upd, li, ds, fin_load<real, KP, MODE>(f, col, upd, li));
+}
+
+// Fused finalisation of an id-like field's row pass over positive segments
+// (the FUSE kernels): deterministic, no float atomics.  A wave walks chunk c
+// of NSG consecutive segments (segments in row order, a row's segments
+// contiguous), one per subgroup, each with its x-scaled output vector `out`.
+// Through the wave's LDS slice (hw: NSG x KP, hr: NSG rows) the first
+// subgroup of each run of same-row segments sums the run in order.  A row
+// whose segments all lie in this chunk is finalised right away (column col);
+// a longer row leaves the run's sum in a slot of chunk c (sc1 stores) and
+// takes a ticket on its column.  A chunk has two slots: 2c+1 for the run of a
+// row that starts in it, 2c for the run of a row that started before it (at
+// most one of each).  When a ticket shows the row's last chunk has arrived,
+// the whole wave sums the row's slots (subgroup t takes chunks c0+t, c0+t+NSG,
+// ... in order, then a fixed cross-subgroup tree; sc1 loads: the guide's
+// last-arriver hand-off) and subgroup 0 finalises: a Pareto-head row of ~1,000
+// segments costs two load rounds, not a serial walk.  Every lane of the wave
+// calls this once per chunk.  lq: 6 words of the wave's LDS.
+template <typename real, int KP, int MODE>
+__device__ __forceinline__ void chunk_finalize(const Fin<real> &f, uint64_t c, int sg, int li, bool valid,
+                                               uint32_t row, vec_t<real> out, uint32_t col,
+                                               const uint32_t *__restrict__ segptr, uint32_t nrow, real *slots,
+                                               uint64_t nchunk, real alpha, real beta, bool upd, double (&ds)[3],
+                                               real *hw, uint32_t *hr, uint32_t *lq) {
+  using G = Geo<real, KP>;
+  constexpr int NSG = G::NSG, VE = G::VE;
+  const int lane = threadIdx.x & 63;
+  *reinterpret_cast<vec_t<real> *>(hw + sg * KP + li * VE) = out;
+  if (li == 0) hr[sg] = valid ? row : 0xffffffffu;
+  if (lane == 0) {
+    lq[0] = 0xffffffffu;  // rows whose last chunk this is: [0] started before c, [1] starts in c
+    lq[3] = 0xffffffffu;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const bool lead = valid && (sg == 0 || hr[sg - 1] != row);
+  if (lead) {
+    vec_t<real> sum = out;
+    for (int t = sg + 1; t < NSG && hr[t] == row; t++)
+      sum += *reinterpret_cast<const vec_t<real> *>(hw + t * KP + li * VE);
+    const uint64_t s0 = segptr[row];
+    const uint64_t c0 = s0 / NSG, c1 = (s0 + nrow - 1) / NSG;
+    if (c0 == c1) {
+      col_finalize<real, KP, MODE>(f, col, sum, alpha, beta, upd, li, ds);
+    } else {
+      const int kind = c == c0 ? 1 : 0;
+      real *sl = slots + (2 * c + kind) * KP + li * VE;
+#pragma unroll
+      for (int e = 0; e < VE; e++) __hip_atomic_store(sl + e, sum[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (li == 0 && __hip_atomic_fetch_add(f.cnt + col, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                         (unsigned)(c1 - c0)) {
+        lq[3 * kind] = row;
+        lq[3 * kind + 1] = col;
+        lq[3 * kind + 2] = nrow;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+  for (int kind = 0; kind < 2; kind++) {
+    const uint32_t lrow = lq[3 * kind];
+    if (lrow == 0xffffffffu) continue;  // wave-uniform
+    const uint32_t lcol = lq[3 * kind + 1], lnrow = lq[3 * kind + 2];
+    const uint64_t s0 = segptr[lrow];
+    const uint64_t c0 = s0 / NSG, c1 = (s0 + lnrow - 1) / NSG;
+    const BufView pv = buf_view(slots, 2 * nchunk * KP * sizeof(real));
+    constexpr int RB = 8;
+    vec_t<real> sum = vzero<real>();
+    for (uint64_t q0 = c0 + sg; q0 <= c1; q0 += (uint64_t)RB * NSG) {
+      vec_t<real> y[RB];
+#pragma unroll
+      for (int u = 0; u < RB; u++) {
+        const uint64_t q = q0 + (uint64_t)u * NSG;
+        const uint64_t slot = 2 * q + (q == c0 ? 1 : 0);
+        const uint32_t off = q <= c1 ? (uint32_t)((slot * KP + li * VE) * sizeof(real)) : pv.oob;
+        y[u] = __builtin_bit_cast(vec_t<real>, __builtin_amdgcn_raw_buffer_load_b128(pv.r, off, 0, 16));
+      }
+#pragma unroll
+      for (int u = 0; u < RB; u++) sum += y[u];  // absent slots read zero
+    }
+    sum = xsg_vsum<G::LPR, real>(sum);  // fixed tree over the subgroups
+    if (sg == 0) {
+      col_finalize<real, KP, MODE>(f, lcol, sum, alpha, beta, upd, li, ds);
+      if (li == 0) __hip_atomic_store(f.cnt + lcol, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the LDS slice is rewritten by the next chunk
 }
 
 // Grid-wide end of a finalising kernel.  MODE 0 publishes g2 and the first
@@ -673,7 +737,7 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
                                                         const int64_t *__restrict__ xptr,
                                                         const uint32_t *__restrict__ xidx,
                                                         const real *__restrict__ xval, uint64_t q1rows,
-                                                        Fin<real> f) {
+                                                        Fin<real> f, const uint32_t *__restrict__ segptr) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP>;
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real)), bb = buf_view(b1, q1rows * sizeof(real));
@@ -696,8 +760,7 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
     bQ[e] = (real)sums[KP + li * G::VE + e];
   }
   double dsum[3] = {0, 0, 0};
-  for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) {
-    const Seg sgm = segs[s];
+  auto body = [&](const Seg &sgm) -> vec_t<real> {
     const uint64_t i = sgm.row;
     const real ai = a1[i];
     vec_t<real> pk = vzero<real>();
@@ -733,16 +796,33 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
       const real z = ai - (real)r;
       pk += vsplat<real>((real)w) * (t + vsplat<real>(z) * oQ + bQ);
     }
-    if (!FUSE) {
-      vst<real>(h + s * KP + li * G::VE, pk);
-    } else {
-      const int64_t xp = xptr[i];
-      const uint32_t d = xidx[xp];
-      pk = vsplat<real>(xval[xp]) * pk;
-      if (col_arrive<real, KP>(f, d, seg_nrow(sgm), pk, sg, li)) col_finalize<real, KP, 0>(f, d, pk, 0, 0, false, li, dsum);
+    return pk;
+  };
+  if constexpr (!FUSE) {
+    for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) vst<real>(h + s * KP + li * G::VE, body(segs[s]));
+  } else {  // id-like field: the row pass finalises its columns (chunk_finalize; h holds the chunk slots)
+    __shared__ __align__(16) real hw[BLOCK / 64][G::NSG * KP];
+    __shared__ uint32_t hr[BLOCK / 64][G::NSG];
+    __shared__ uint32_t lq[BLOCK / 64][6];
+    const int wv = threadIdx.x >> 6;
+    const uint64_t nchunk = (nseg + G::NSG - 1) / G::NSG;
+    for (uint64_t c = wave; c < nchunk; c += nwaves) {
+      const uint64_t s = c * G::NSG + sg;
+      const bool valid = s < nseg;
+      vec_t<real> out = vzero<real>();
+      uint32_t row = 0, col = 0, nrow = 1;
+      if (valid) {
+        const Seg sgm = segs[s];
+        row = sgm.row;
+        nrow = seg_nrow(sgm);
+        col = xidx[row];  // id-like: one node per row
+        out = vsplat<real>(xval[row]) * body(sgm);
+      }
+      chunk_finalize<real, KP, 0>(f, c, sg, li, valid, row, out, col, segptr, nrow, h, nchunk, (real)0, (real)0, false,
+                                  dsum, hw[wv], hr[wv], lq[wv]);
     }
+    fin_blocks<real, 0>(f, dsum);
   }
-  if (FUSE) fin_blocks<real, 0>(f, dsum);
 }
 
 // Per segment: h[s] = zpart * q1_i, zpart = sum_{p in seg} ((1-w) y~ - w (1-r))
@@ -757,7 +837,8 @@ __global__ __launch_bounds__(BLOCK) void k_gd_side_seg(uint64_t nseg, const Seg 
                                                        double r, real *__restrict__ h,
                                                        const int64_t *__restrict__ xptr,
                                                        const uint32_t *__restrict__ xidx,
-                                                       const real *__restrict__ xval, uint64_t nb1, Fin<real> f) {
+                                                       const real *__restrict__ xval, uint64_t nb1, Fin<real> f,
+                                                       const uint32_t *__restrict__ segptr) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP>;
   const BufView bb = buf_view(b1, nb1 * sizeof(real));
@@ -766,8 +847,7 @@ __global__ __launch_bounds__(BLOCK) void k_gd_side_seg(uint64_t nseg, const Seg 
   const real cpos = (real)(1 - w), cneg = (real)(w * (1 - r));
   const double bs = *bsum;
   double dsum[3] = {0, 0, 0};
-  for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) {
-    const Seg sgm = segs[s];
+  auto body = [&](const Seg &sgm) -> vec_t<real> {
     const uint64_t i = sgm.row;
     const real ai = a1[i];
     real z = 0;
@@ -787,17 +867,33 @@ __global__ __launch_bounds__(BLOCK) void k_gd_side_seg(uint64_t nseg, const Seg 
     }
     z = sg_sum<G::LPR>(z);
     if (seg_first(sgm)) z += (real)(w * (n1 * ((double)ai - r) + bs + (double)sa1[i]));
-    vec_t<real> out = vsplat<real>(z) * vld<real>(Q1 + i * KP + li * G::VE);
-    if (!FUSE) {
-      vst<real>(h + s * KP + li * G::VE, out);
-    } else {
-      const int64_t xp = xptr[i];
-      const uint32_t d = xidx[xp];
-      out = vsplat<real>(xval[xp]) * out;
-      if (col_arrive<real, KP>(f, d, seg_nrow(sgm), out, sg, li)) col_finalize<real, KP, 0>(f, d, out, 0, 0, false, li, dsum);
+    return vsplat<real>(z) * vld<real>(Q1 + i * KP + li * G::VE);
+  };
+  if constexpr (!FUSE) {
+    for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) vst<real>(h + s * KP + li * G::VE, body(segs[s]));
+  } else {  // id-like field: the row pass finalises its columns (chunk_finalize)
+    __shared__ __align__(16) real hw[BLOCK / 64][G::NSG * KP];
+    __shared__ uint32_t hr[BLOCK / 64][G::NSG];
+    __shared__ uint32_t lq[BLOCK / 64][6];
+    const int wv = threadIdx.x >> 6;
+    const uint64_t nchunk = (nseg + G::NSG - 1) / G::NSG;
+    for (uint64_t c = wave; c < nchunk; c += nwaves) {
+      const uint64_t s = c * G::NSG + sg;
+      const bool valid = s < nseg;
+      vec_t<real> out = vzero<real>();
+      uint32_t row = 0, col = 0, nrow = 1;
+      if (valid) {
+        const Seg sgm = segs[s];
+        row = sgm.row;
+        nrow = seg_nrow(sgm);
+        col = xidx[row];
+        out = vsplat<real>(xval[row]) * body(sgm);
+      }
+      chunk_finalize<real, KP, 0>(f, c, sg, li, valid, row, out, col, segptr, nrow, h, nchunk, (real)0, (real)0, false,
+                                  dsum, hw[wv], hr[wv], lq[wv]);
     }
+    fin_blocks<real, 0>(f, dsum);
   }
-  if (FUSE) fin_blocks<real, 0>(f, dsum);
 }
 
 // ------------------------------------------------ Hessian-vector rows ---
@@ -997,7 +1093,8 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
                                                         const int *__restrict__ run, const real *__restrict__ Rv,
                                                         const real *__restrict__ Hv, const CgState *st, int it,
                                                         const uint32_t *__restrict__ segd,
-                                                        const real *__restrict__ segx, Fin<real> f) {
+                                                        const real *__restrict__ segx, Fin<real> f,
+                                                        const uint32_t *__restrict__ segptr) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP, 32>;  // one round of gathers per <= 32-positive segment
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real));
@@ -1017,31 +1114,8 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
   const int sg = lane / G::LPR, li = lane % G::LPR;
   const real cpos = (real)(1 - w);
   double dsum[3] = {0, 0, 0};
-  // Grid-stride over segments with the next segment's descriptor (and its
-  // node) in flight while the current one is gathered.
-  const uint64_t stride = nwaves * G::NSG;
-  uint64_t s = wave * G::NSG + sg;
-  Seg nxt{0u, 0u, 0, 0};
-  uint32_t nd = 0;
-  real nx = 0;
-  if (s < nseg) {
-    nxt = segs[s];
-    if (segd) {
-      nd = segd[s];
-      nx = segx[s];
-    }
-  }
-  for (; s < nseg; s += stride) {
-    const Seg sgm = nxt;
-    const uint32_t d1 = nd;
-    const real x1 = nx;
-    if (s + stride < nseg) {
-      nxt = segs[s + stride];
-      if (segd) {
-        nd = segd[s + stride];
-        nx = segx[s + stride];
-      }
-    }
+  // Per segment: phi from the row's node(s), the partner-row gathers, tau.
+  auto seg_out = [&](const Seg &sgm, uint32_t d1, real x1) -> vec_t<real> {
     const uint64_t i = sgm.row;
     uint32_t jj[PP::UT];  // the first pass's columns go out with the phi gather
     PP::load_cols(ycol, sgm.b, sgm.e, li, jj);
@@ -1074,17 +1148,61 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
     if (QTQ && seg_first(sgm)) {
       out += vsplat<real>((real)w) * sg_vecmat<real, KP>(phi, Qp, li);
     }
-    if (!FUSE) {
-      vst<real>(h + s * KP + li * G::VE, out);
-    } else {
-      const int64_t xp = xptr[i];
-      const uint32_t d = xidx[xp];
-      out = vsplat<real>(xval[xp]) * out;
-      if (col_arrive<real, KP>(f, d, seg_nrow(sgm), out, sg, li)) col_finalize<real, KP, 1>(f, d, out, alpha, beta, upd, li, dsum);
+    return out;
+  };
+  if constexpr (FUSE) {  // id-like field: the row pass finalises its columns (chunk_finalize)
+    __shared__ __align__(16) real hw[BLOCK / 64][G::NSG * KP];
+    __shared__ uint32_t hr[BLOCK / 64][G::NSG];
+    __shared__ uint32_t lq[BLOCK / 64][6];
+    const int wv = threadIdx.x >> 6;
+    const uint64_t nchunk = (nseg + G::NSG - 1) / G::NSG;
+    for (uint64_t c = wave; c < nchunk; c += nwaves) {
+      const uint64_t s = c * G::NSG + sg;
+      const bool valid = s < nseg;
+      vec_t<real> out = vzero<real>();
+      uint32_t row = 0, col = 0, nrow = 1;
+      if (valid) {
+        const Seg sgm = segs[s];
+        row = sgm.row;
+        nrow = seg_nrow(sgm);
+        col = segd[s];
+        out = vsplat<real>(segx[s]) * seg_out(sgm, col, segx[s]);
+      }
+      chunk_finalize<real, KP, 1>(f, c, sg, li, valid, row, out, col, segptr, nrow, h, nchunk, alpha, beta, upd, dsum,
+                                  hw[wv], hr[wv], lq[wv]);
+    }
+    fin_blocks<real, 1>(f, dsum);
+    return;
+  }
+  // Grid-stride over segments with the next segment's descriptor (and its
+  // node) in flight while the current one is gathered.
+  const uint64_t stride = nwaves * G::NSG;
+  uint64_t s = wave * G::NSG + sg;
+  Seg nxt{0u, 0u, 0, 0};
+  uint32_t nd = 0;
+  real nx = 0;
+  if (s < nseg) {
+    nxt = segs[s];
+    if (segd) {
+      nd = segd[s];
+      nx = segx[s];
     }
   }
-  if (FUSE) fin_blocks<real, 1>(f, dsum);
+  for (; s < nseg; s += stride) {
+    const Seg sgm = nxt;
+    const uint32_t d1 = nd;
+    const real x1 = nx;
+    if (s + stride < nseg) {
+      nxt = segs[s + stride];
+      if (segd) {
+        nd = segd[s + stride];
+        nx = segx[s + stride];
+      }
+    }
+    vst<real>(h + s * KP + li * G::VE, seg_out(sgm, d1, x1));
+  }
 }
+
 
 // ------------------------------------------- row-complete cross halves ---
 // Id-like field, one GPU, fp32, KP = 32 ("row-complete"): every

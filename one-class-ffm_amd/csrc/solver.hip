@@ -375,7 +375,11 @@ template <typename real> class Problem final : public ProblemBase {
     Vd_.alloc(dk);
     Rv_.alloc(dk);
     Hv_.alloc(dk);
-    h_.alloc(std::max<uint64_t>(std::max(Rmax, std::max(U_.nseg, V_.nseg)), 1) * kp_);
+    // h: row or segment partials; the fused id-field passes use it for two
+    // slots per wave-chunk of segments (kernels.hpp chunk_finalize)
+    const uint64_t nsegmax = std::max(U_.nseg, V_.nseg);
+    const uint64_t nslots = 2 * ((nsegmax + nsg() - 1) / nsg());
+    h_.alloc(std::max<uint64_t>(std::max(Rmax, std::max(nsegmax, nslots)), 1) * kp_);
     if (std::max(U_.R, V_.R) * kp_ * sizeof(real) >= (1ull << 32) - 64)  // partner-row gathers (BufView)
       throw Error(OCFFM_E_DATA, "too many rows per GPU for 32-bit gather offsets; shard over more GPUs");
     if (std::max(U_.npos, V_.npos) * 4 >= (1ull << 32) - 64)  // column reads through a BufView (k_hs_cross_w)
@@ -1345,7 +1349,7 @@ template <typename real> class Problem final : public ProblemBase {
           launch(k_gd_cross_seg<real, KP, ML, FZ>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, ML ? msz : 0,
               own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
               (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, h.partner->bias.p, w_,
-              r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, (uint64_t)h.partner->R, fin);
+              r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, (uint64_t)h.partner->R, fin, (const uint32_t *)own.segptr.p);
         };
         prof_launch(fz_ ? "gd_cross_fused" : "gd_cross_row", bytes, [&] {
           if (fz_) {
@@ -1370,7 +1374,7 @@ template <typename real> class Problem final : public ProblemBase {
           constexpr bool FZ = decltype(fz)::value;
           launch(k_gd_side_seg<real, KP, FZ>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, 0,
               own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, own.bias.p, other.bias.p, own.s.p, bsum_.p + (h.user ? 1 : 0),
-              n1, w_, r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, (uint64_t)other.R, fin);
+              n1, w_, r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, (uint64_t)other.R, fin, (const uint32_t *)own.segptr.p);
         };
         prof_launch(fz_ ? "gd_side_fused" : "gd_side_row", bytes, [&] {
           if (fz_) go(std::true_type());
@@ -1512,9 +1516,11 @@ template <typename real> class Problem final : public ProblemBase {
   }
 
   // fuse_ 1: the Hessian-vector pass of side halves only (one row = one
-  // feature, no partial sums); 2: every row pass (the gradient passes and the
-  // cross halves walk positive segments, whose multi-segment rows meet through
-  // column atomics: slower on Pareto-headed items).
+  // feature, no partial sums); 2: every row pass of an id-like field (the
+  // gradient passes and the cross halves walk positive segments: a row's
+  // segments meet in the wave's LDS, or through ordered chunk slots and a
+  // last-arriver sum when the row spans several chunks, kernels.hpp
+  // chunk_finalize).
   bool fused_rows(const HalfCtx &h, bool hv) const {
     return h.F->idlike && !comm_.active() && (fuse_ >= 2 || (fuse_ == 1 && hv && !h.cross));
   }
@@ -1653,7 +1659,7 @@ template <typename real> class Problem final : public ProblemBase {
             constexpr bool FZ = decltype(fz)::value, ML = decltype(ml)::value;
             launch(k_hs_cross_seg<real, KP, ML, FZ>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : hs_blocks_), BLOCK, smem, own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p,
                                                          own.ycol.p, h.Q1, (uint64_t)h.partner->R, coltau(h) ? (const real *)nullptr : (const real *)qtq_, w_, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
-                                                         F.segd.p, F.segx.p, fin);
+                                                         F.segd.p, F.segx.p, fin, (const uint32_t *)own.segptr.p);
           };
           prof_launch(fz_ ? "hs_cross_fused" : "hs_cross_row", bytes, [&] {
             if (fz_) {

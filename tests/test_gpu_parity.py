@@ -271,7 +271,7 @@ def test_heavy_columns(precision, cgram, monkeypatch):
         assert abs(gpu_objective(o2, g) - f_ref) <= 1e-3 * abs(f_ref)
 
 
-@pytest.mark.parametrize("ds_name", ["heavy", "kkbox_s"])
+@pytest.mark.parametrize("ds_name", ["heavy", "kkbox_s", "kkbox_s_fuse2"])
 def test_fp32_runs_bit_identical(ds_name, monkeypatch):
     """The default fp32 path has no order-dependent float sums (feature
     passes, Gram builds and grid reductions combine in a fixed order): two
@@ -281,6 +281,8 @@ def test_fp32_runs_bit_identical(ds_name, monkeypatch):
         monkeypatch.setenv("OCFFM_CGRAM", "2")
         ds = synth.general(**HEAVY)
     else:
+        if ds_name.endswith("fuse2"):  # id-like row passes finalise their columns (chunk_finalize)
+            monkeypatch.setenv("OCFFM_FUSE", "2")
         ds = synth.kkbox(m=3000, n=4000, mean=20.0, seed=11, name="kk_det")
     runs = []
     for _ in range(2):

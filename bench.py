@@ -79,6 +79,10 @@ def main():
         obj = [ocffm.comm_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         comm = obj[0]
+    elif os.environ.get("OCFFM_BENCH_COMM1") == "1":
+        # N = 1 on the multi-rank code path (a one-rank RCCL communicator):
+        # the compute cost of that path without any real exchange
+        comm = ocffm.comm_id()
     g = ocffm.problem_from_dataset(ds, precision=prec, with_test=False, device=local, rank=rank, nranks=world,
                                    comm=comm, allreduce=allreduce)
     ocffm.srand(1)
@@ -165,7 +169,8 @@ def main():
                        "rows_per_gpu": ROWS_PER_GPU, "rows_total": rows_total, "items": int(ds.item.m),
                        "positives": ds.n_positives, "user_fields": 2, "item_fields": 3, "k": 32,
                        "lambda": 4.0, "omega": 0.0078125, "r": -1.0,
-                       "parallelism": f"dp{world}", "cg_iters_per_epoch": round(cg.sum() / max(1, args.steps), 1)},
+                       "parallelism": f"dp{world}" + ("-rccl1" if comm is not None and world == 1 else ""),
+                       "cg_iters_per_epoch": round(cg.sum() / max(1, args.steps), 1)},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

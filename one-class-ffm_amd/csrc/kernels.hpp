@@ -1058,8 +1058,10 @@ __global__ __launch_bounds__(BLOCK) void k_col_gram(const Job *__restrict__ chun
 
 // One CG step of a Gram side half: per column, the direction p_c of
 // iteration f.it (formed from r, Hp, p as col_finalize does), s = G_c p_c,
-// then the Hessian-vector finalisation (MODE 1).  One column per subgroup.
-template <typename real, int KP>
+// then the Hessian-vector finalisation (MODE 1), or s stored into f.acc for
+// the all-reduce of several ranks (MODE 2: the Grams are partials over this
+// rank's positives and rows).  One column per subgroup.
+template <typename real, int KP, int MODE = 1>
 __global__ __launch_bounds__(BLOCK) void k_hv_cgram(uint64_t D, const real *__restrict__ G, Fin<real> f) {
   using Gm = Geo<real, KP>;
   if (!f.st->run[f.it]) return;
@@ -1073,9 +1075,10 @@ __global__ __launch_bounds__(BLOCK) void k_hv_cgram(uint64_t D, const real *__re
     vec_t<real> pt = ops.w_or_p;
     if (upd) pt = (ops.r - vsplat<real>(alpha) * ops.hp) + vsplat<real>(beta) * ops.w_or_p;
     const vec_t<real> s = sg_vecmat<real, KP>(pt, G + c * KP * KP, li);
-    col_finalize<real, KP, 1>(f, (uint32_t)c, s, alpha, beta, upd, li, dsum, ops);
+    if constexpr (MODE == 2) vst<real>(f.acc + c * KP + li * Gm::VE, s);
+    else col_finalize<real, KP, 1>(f, (uint32_t)c, s, alpha, beta, upd, li, dsum, ops);
   }
-  fin_blocks<real, 1>(f, dsum);
+  if constexpr (MODE != 2) fin_blocks<real, 1>(f, dsum);
 }
 
 // Per segment of row i: h[s] = (1-w) sum_{j in seg} <phi_i, q_j> q_j
@@ -1371,7 +1374,8 @@ __global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__res
                                                 Fin<real> f, const real *__restrict__ QTQ) {
   using G = Geo<real, KP>;
   if (f.it > 0 && !f.st->run[f.it]) return;
-  // TAU (MODE 1): QTQ staged in LDS for the per-column tau term
+  // TAU (MODE 1, and MODE 2 on several ranks): QTQ staged in LDS for the
+  // per-column tau term (MODE 2 forms the column's CG direction for it)
   extern __shared__ __align__(16) unsigned char smem_raw[];
   real *Qs = reinterpret_cast<real *>(smem_raw);
   if constexpr (TAU) {
@@ -1379,7 +1383,7 @@ __global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__res
     __syncthreads();
   }
   const BufView hb = buf_view(h, hbytes);
-  const bool upd = MODE == 1 && f.it > 1;
+  const bool upd = (MODE == 1 || (MODE == 2 && TAU)) && f.it > 1;
   const real alpha = upd ? (real)f.st->alpha : (real)0, beta = upd ? (real)f.st->beta : (real)0;
   const int lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
@@ -1448,8 +1452,13 @@ __global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__res
       }
     }
     if (mine) {
-      if (MODE == 2) vst<real>(f.acc + (size_t)jb.col * KP + li * G::VE, s);
-      else col_finalize<real, KP, (MODE == 2 ? 0 : MODE), TAU>(f, jb.col, s, alpha, beta, upd, li, dsum, ops, Qs);
+      if constexpr (MODE == 2) {
+        if constexpr (TAU) {
+          const vec_t<real> d = cg_dir_at<real, KP>(f.P, f.R, f.Hp, alpha, beta, upd, (size_t)jb.col * KP + li * G::VE);
+          s += vsplat<real>((real)(f.tw * (double)f.xsq[jb.col])) * sg_vecmat<real, KP>(d, Qs, li);
+        }
+        vst<real>(f.acc + (size_t)jb.col * KP + li * G::VE, s);
+      } else col_finalize<real, KP, (MODE == 2 ? 0 : MODE), TAU>(f, jb.col, s, alpha, beta, upd, li, dsum, ops, Qs);
     }
   }
   if (MODE != 2) fin_blocks<real, (MODE == 2 ? 0 : MODE)>(f, dsum);

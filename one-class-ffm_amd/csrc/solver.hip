@@ -898,8 +898,8 @@ template <typename real> class Problem final : public ProblemBase {
       F->jobs.upload(jobs);
       F->njw = jobs.size() / nsg();
       F->cnt.alloc(std::max<uint64_t>(F->D, 1));
-      if (F->one && !F->idlike && cgram_on_ && R > 0 && prm_.self_side && !comm_.active() &&
-          cgram_pays(R, F->D) && F->D * kp_ * kp_ * sizeof(real) <= (1ull << 30))
+      if (F->one && !F->idlike && !F->excl && cgram_on_ && R > 0 && prm_.self_side && cgram_pays(R, F->D) &&
+          F->D * kp_ * kp_ * sizeof(real) <= (1ull << 30))
         col_gram_chunks(*F, xidx);
       F->h_xptr = std::move(xptr);
       F->h_xidx = std::move(xidx);
@@ -1459,8 +1459,9 @@ template <typename real> class Problem final : public ProblemBase {
     F.gslots = slots;
   }
 
-  // Side half whose CG steps run on per-column Grams (one GPU).
-  bool cgram(const HalfCtx &h) const { return !h.cross && h.F->gchunks.n && !comm_.active(); }
+  // Side half whose CG steps run on per-column Grams (several ranks: each
+  // builds its partial Grams, and every CG step all-reduces G_c p_c).
+  bool cgram(const HalfCtx &h) const { return !h.cross && h.F->gchunks.n; }
 
   // Does a side half over a one-node-per-row field (R rows, D columns) pay
   // for its Grams?  Estimated time (us) of a half of `c` CG steps, from the
@@ -1507,11 +1508,13 @@ template <typename real> class Problem final : public ProblemBase {
   // for a one-node-per-row field, is w (sum_{i in col d} x_i^2) p_d QTQ per
   // column, added by the feature pass (k_feat TAU) instead of per row by
   // k_hs_cross_seg: one k x k product per column instead of per row (items
-  // over artist / genre: 100,000 rows, 5,000 / 50 columns).  One GPU (on
-  // several ranks the item halves' QTQ is a partial over local users).
+  // over artist / genre: 100,000 rows, 5,000 / 50 columns).  On several ranks
+  // the term is added to the column partial sums before the all-reduce (it is
+  // linear in QTQ, a partial over local users on the item halves, and in
+  // sum x^2, a partial over local rows on the user halves).
   static constexpr size_t COLTAU_LDS = 32 * 1024;
   bool coltau(const HalfCtx &h) const {
-    return coltau_on_ && h.cross && h.F->one && !comm_.active() && !fused_rows(h, true) && !row_complete(h) &&
+    return coltau_on_ && h.cross && h.F->one && !fused_rows(h, true) && !row_complete(h) &&
            (size_t)kp_ * kp_ * sizeof(real) <= COLTAU_LDS;
   }
 
@@ -1567,6 +1570,14 @@ template <typename real> class Problem final : public ProblemBase {
           }
           launch(k_feat<real, KP, 1>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, fin, nq);
         } else {
+          if constexpr ((size_t)KP * KP * sizeof(real) <= COLTAU_LDS) {
+            if (coltau(h) && it > 0) {
+              fin.xsq = F.xsq.p;
+              launch(k_feat<real, KP, 2, JOB_ENT, true>, grid, BLOCK, (size_t)KP * KP * sizeof(real), njw, jobs, crow,
+                     cval, h_.p, h_.bytes(), wpart_.p, fin, (const real *)qtq_);
+              return;
+            }
+          }
           launch(k_feat<real, KP, 2>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, fin, nq);
         }
       });
@@ -1634,10 +1645,21 @@ template <typename real> class Problem final : public ProblemBase {
         using Gm = Geo<real, KP>;
         const double rs = sizeof(real);
         const Fin<real> fin = make_fin(h, it);
-        prof_launch("hv_cgram", (double)h.D * KP * KP * rs + (double)h.D * KP * rs * (it > 1 ? 9 : 4), [&] {
-          launch(k_hv_cgram<real, KP>, grid_for(h.D, 4 * Gm::NSG, 1024), BLOCK, 0, (uint64_t)h.D,
+        if (!comm_.active()) {
+          prof_launch("hv_cgram", (double)h.D * KP * KP * rs + (double)h.D * KP * rs * (it > 1 ? 9 : 4), [&] {
+            launch(k_hv_cgram<real, KP>, grid_for(h.D, 4 * Gm::NSG, 1024), BLOCK, 0, (uint64_t)h.D,
+                   (const real *)h.F->gram.p, fin);
+          });
+          return;
+        }
+        prof_launch("hv_cgram", (double)h.D * KP * KP * rs + (double)h.D * KP * rs * 4, [&] {
+          launch(k_hv_cgram<real, KP, 2>, grid_for(h.D, 4 * Gm::NSG, 1024), BLOCK, 0, (uint64_t)h.D,
                  (const real *)h.F->gram.p, fin);
         });
+        allreduce_dev(acc_.p, h.D * kp_);
+        const uint64_t nv = h.D * KP / Gm::VE;
+        prof_launch("hv_fin", (double)h.D * KP * rs * (it > 1 ? 9 : 4),
+                    [&] { launch(k_fin<real, KP, 1>, grid_for(nv, BLOCK, 2048), BLOCK, 0, nv, fin); });
       });
       return;
     }

@@ -9,5 +9,5 @@ steps=${3:-10}
 mkdir -p gpurun_out
 for v in $vals; do
   env $var=$v timeout -k 10 300 python bench.py --steps $steps --warmup 2 --cpu-baseline off --sgd off > gpurun_out/sweep_${var}_$v.json 2> gpurun_out/sweep_${var}_$v.err
-  python -c "import json,sys; d=json.load(open('gpurun_out/sweep_${var}_$v.json')); r=d['roofline']; print('$var=$v', d['ms_per_step'], 'ms/step', r['kernel'], r['avg_launch_us'], 'us', 'frac', r['frac'])"
+  python -c "import json,sys; d=json.loads(open('gpurun_out/sweep_${var}_$v.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$var=$v', d['ms_per_step'], 'ms/step', r['kernel'], r['avg_launch_us'], 'us', 'frac', r['frac'])"
 done

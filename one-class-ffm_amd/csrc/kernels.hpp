@@ -899,7 +899,9 @@ __global__ __launch_bounds__(BLOCK) void k_gd_side_seg(uint64_t nseg, const Seg 
 // ------------------------------------------------ Hessian-vector rows ---
 // h_i = d_i <phi_i, q1_i> q1_i, phi_i = X_i V, d_i = (1-w)|pos(i)| + w n1
 // (hs_side row body, ffm.cpp:603-624).  One row per subgroup, row-indexed h.
-template <typename real, int KP, bool FUSE>
+// SCAT (id-like field, several ranks): x_i h_i goes straight to its column's
+// slot of f.acc for the all-reduce (the CSC scatter is the identity).
+template <typename real, int KP, bool FUSE, bool SCAT = false>
 __global__ __launch_bounds__(BLOCK) void k_hs_side_row(uint64_t R, const int64_t *__restrict__ xptr,
                                                        const uint32_t *__restrict__ xidx,
                                                        const real *__restrict__ xval, const real *__restrict__ V,
@@ -941,7 +943,11 @@ __global__ __launch_bounds__(BLOCK) void k_hs_side_row(uint64_t R, const int64_t
     const vec_t<real> q = vld<real>(Q1 + i * KP + li * G::VE);
     const real z = sg_sum<G::LPR>(hsum<real>(phi * q));
     const real d = (real)((1 - w) * (double)(yptr[i + 1] - yptr[i]) + w * n1);
-    vst<real>(h + i * KP + li * G::VE, vsplat<real>(d * z) * q);
+    if constexpr (SCAT) {  // id-like field on several ranks: row i is column xidx[i]'s only row
+      vst<real>(f.acc + (size_t)xidx[i] * KP + li * G::VE, vsplat<real>(xval[i] * d * z) * q);
+    } else {
+      vst<real>(h + i * KP + li * G::VE, vsplat<real>(d * z) * q);
+    }
   }
   if (FUSE) fin_blocks<real, 1>(f, dsum);
 }

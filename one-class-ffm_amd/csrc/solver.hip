@@ -1528,6 +1528,11 @@ template <typename real> class Problem final : public ProblemBase {
     return h.F->idlike && !comm_.active() && (fuse_ >= 2 || (fuse_ == 1 && hv && !h.cross));
   }
 
+  // Several ranks, id-like field (replicated rows, e.g. items; never an owned
+  // field): the side Hessian-vector row pass writes its column partials
+  // straight into acc (k_hs_side_row SCAT), no CSC scatter launch.
+  bool scat_rows(const HalfCtx &h) const { return comm_.active() && h.F->idlike && !h.F->excl && !h.cross; }
+
   void scatter(HalfCtx &h, int it, bool seg) {
     DevField<real> &F = *h.F;
     feat_launch(h, it, seg, 2);
@@ -1587,7 +1592,7 @@ template <typename real> class Problem final : public ProblemBase {
   // Feature pass of a half: fused gather + finalisation on one GPU; gather,
   // all-reduce, finalisation when the partial sums must meet across ranks.
   // mode 0: gradient (it = 0), mode 1: Hessian-vector of CG iteration `it`.
-  void feature_pass(HalfCtx &h, int it, bool seg) {
+  void feature_pass(HalfCtx &h, int it, bool seg, bool acc_ready = false) {
     if (!comm_.active()) {
       feat_launch(h, it, seg, it == 0 ? 0 : 1);
       return;
@@ -1603,7 +1608,8 @@ template <typename real> class Problem final : public ProblemBase {
       });
       return;
     }
-    scatter(h, it, seg);
+    if (acc_ready) allreduce_dev(acc_.p, h.F->D * kp_);  // the row pass filled acc (scat_rows)
+    else scatter(h, it, seg);
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
       using Gm = Geo<real, KP>;
@@ -1697,20 +1703,21 @@ template <typename real> class Problem final : public ProblemBase {
           const double n1 = (double)other.R;
           const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
                                (double)own.R * KP * rs * 2;
-          auto go = [&](auto fz) {
-            constexpr bool FZ = decltype(fz)::value;
-            launch(k_hs_side_row<real, KP, FZ>, grid_for(own.R, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, 0,
+          auto go = [&](auto fz, auto sc) {
+            constexpr bool FZ = decltype(fz)::value, SC = decltype(sc)::value;
+            launch(k_hs_side_row<real, KP, FZ, SC>, grid_for(own.R, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, 0,
                 own.R, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.yptr.p, h.Q1, w_, n1, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
                 F.one, fin);
           };
           prof_launch(fz_ ? "hs_side_fused" : "hs_side_row", bytes, [&] {
-            if (fz_) go(std::true_type());
-            else go(std::false_type());
+            if (fz_) go(std::true_type(), std::false_type());
+            else if (scat_rows(h)) go(std::false_type(), std::true_type());
+            else go(std::false_type(), std::false_type());
           });
         }
       }
     });
-    if (!fz_) feature_pass(h, it, h.cross);
+    if (!fz_) feature_pass(h, it, h.cross, !h.cross && scat_rows(h));
   }
 
   // One half of a block: gradient, Newton-CG, update (ffm.cpp:826-832, 843-849).

@@ -729,7 +729,7 @@ __global__ __launch_bounds__(BLOCK) void k_init_ytilde(uint64_t R, const int64_t
 template <typename real, int KP, bool MLDS, bool FUSE>
 __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                         const uint32_t *__restrict__ ycol,
-                                                        const real *__restrict__ yt, const real *__restrict__ Q1,
+                                                        real *__restrict__ yt, const real *__restrict__ Q1,
                                                         int C, const real *const *__restrict__ Ptabs,
                                                         const real *__restrict__ M, const double *__restrict__ sums,
                                                         const real *__restrict__ a1, const real *__restrict__ b1,
@@ -737,10 +737,14 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
                                                         const int64_t *__restrict__ xptr,
                                                         const uint32_t *__restrict__ xidx,
                                                         const real *__restrict__ xval, uint64_t q1rows,
-                                                        Fin<real> f, const uint32_t *__restrict__ segptr) {
+                                                        Fin<real> f, const uint32_t *__restrict__ segptr,
+                                                        const real *__restrict__ drow,
+                                                        const real *__restrict__ dxs, real *__restrict__ yt_other,
+                                                        const uint32_t *__restrict__ perm) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP>;
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real)), bb = buf_view(b1, q1rows * sizeof(real));
+  const BufView xb = buf_view(dxs, dxs ? q1rows * KP * sizeof(real) : 0);
   extern __shared__ __align__(16) unsigned char smem_raw[];
   real *Ms = reinterpret_cast<real *>(smem_raw);
   const real *Mp = M;
@@ -760,10 +764,14 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
     bQ[e] = (real)sums[KP + li * G::VE + e];
   }
   double dsum[3] = {0, 0, 0};
+  // dxs (deferred base update of the previous cross half):
+  // base_ij += <drow_i, dxs_j> is applied here, on the fly, and the new base is
+  // stored in both orientations (this one in place, the other through perm).
   auto body = [&](const Seg &sgm) -> vec_t<real> {
     const uint64_t i = sgm.row;
     const real ai = a1[i];
     vec_t<real> pk = vzero<real>();
+    const vec_t<real> dr = dxs ? vld<real>(drow + i * KP + li * G::VE) : vzero<real>();
     for (int64_t p0 = sgm.b; p0 < sgm.e; p0 += PP::PW) {
       uint32_t jj[PP::UT];
       real yv[PP::UT];
@@ -773,10 +781,13 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
         const int64_t q = p0 + li + t * G::LPR;
         yv[t] = q < sgm.e ? yt[q] : (real)0;
       }
+      real yn[PP::UT];  // dxs: the new base of this lane's positions
+#pragma unroll
+      for (int t = 0; t < PP::UT; t++) yn[t] = yv[t];
       sfor<PP::PW / PP::GB>([&](auto BT) {
         constexpr int bt = decltype(BT)::value * PP::GB;
         if (p0 + bt >= sgm.e) return;
-        vec_t<real> qv[PP::GB];
+        vec_t<real> qv[PP::GB], xv[PP::GB];
         real cb[PP::GB], yb[PP::GB];
         sfor<PP::GB>([&](auto U) {
           constexpr int u = decltype(U)::value;
@@ -784,10 +795,28 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
           yb[u] = PP::template at<bt + u>(yv, li);
           qv[u] = bld<real>(qb, PP::row_off(j, qb, li));
           cb[u] = bld1<real>(bb, j == POS_NONE ? bb.oob : j * (uint32_t)sizeof(real));
+          if (dxs) xv[u] = bld<real>(xb, PP::row_off(j, xb, li));
         });
+        if (dxs) {
+#pragma unroll
+          for (int u = 0; u < PP::GB; u++) {
+            yb[u] += sg_sum<G::LPR>(hsum<real>(dr * xv[u]));
+            if ((bt + u) % G::LPR == li) yn[(bt + u) / G::LPR] = yb[u];
+          }
+        }
 #pragma unroll
         for (int u = 0; u < PP::GB; u++) pk += vsplat<real>(cpos * (yb[u] + ai + cb[u]) - cneg) * qv[u];
       });
+      if (dxs) {
+#pragma unroll
+        for (int t = 0; t < PP::UT; t++) {
+          const int64_t q = p0 + li + t * G::LPR;
+          if (q < sgm.e) {
+            yt[q] = yn[t];
+            if (yt_other) yt_other[perm[q]] = yn[t];
+          }
+        }
+      }
     }
     if (seg_first(sgm)) {
       vec_t<real> t = vzero<real>();
@@ -1549,7 +1578,8 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
                                                             const real *__restrict__ segx,
                                                             real *__restrict__ yt_other,
                                                             const uint32_t *__restrict__ perm, real *__restrict__ W,
-                                                            const real *__restrict__ Pd, const CgState *st) {
+                                                            const real *__restrict__ Pd, const CgState *st,
+                                                            const real *__restrict__ XSin) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP>;
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real));
@@ -1560,7 +1590,9 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
     const Seg sgm = segs[s];
     const uint64_t i = sgm.row;
     vec_t<real> xs = vzero<real>();
-    if (W) {  // id-like field (segd set): the row's first segment does its feature's k_apply work
+    if (XSin) {  // flush of a deferred base update: XS given, P already updated
+      xs = vld<real>(XSin + i * KP + li * G::VE);
+    } else if (W) {  // id-like field (segd set): the row's first segment does its feature's k_apply work
       const size_t off = (size_t)segd[s] * KP + li * G::VE;
       const vec_t<real> sf = seg_first(sgm) ? apply_owned_row<real, KP>(S, Pd, W, alpha, off)
                                             : vld<real>(S + off) + vsplat<real>(alpha) * vld<real>(Pd + off);
@@ -1571,7 +1603,7 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
       for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
         xs += vsplat<real>(xval[p]) * vld<real>(S + (size_t)xidx[p] * KP + li * G::VE);
     }
-    if (seg_first(sgm)) vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
+    if (seg_first(sgm) && !XSin) vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
     for (int64_t p0 = sgm.b; p0 < sgm.e; p0 += PP::PW) {
       uint32_t jj[PP::UT];
       PP::load_cols(ycol, p0, sgm.e, li, jj);
@@ -1614,6 +1646,36 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
         }
       }
     }
+  }
+}
+
+// The cross update without its positive pass (deferred base update, DESIGN
+// §2): XS_i = X_i S, P_i += XS_i, and XS kept for the next cross half's
+// gradient pass, which applies base_ij += <XS_i, q_j> on the fly.  W
+// non-null (id-like field): the row also does its feature's k_apply work.
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_update_cross_rows(uint64_t R, const int64_t *__restrict__ xptr,
+                                                             const uint32_t *__restrict__ xidx,
+                                                             const real *__restrict__ xval,
+                                                             const real *__restrict__ S, real *__restrict__ P1,
+                                                             real *__restrict__ XS, bool one, real *__restrict__ W,
+                                                             const real *__restrict__ Pd, const CgState *st) {
+  using G = Geo<real, KP>;
+  WAVE_SETUP
+  const int sg = lane / G::LPR, li = lane % G::LPR;
+  const real alpha = (W && st->nr_cg >= 1) ? (real)st->alpha : (real)0;
+  for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
+    vec_t<real> xs = vzero<real>();
+    if (W) {
+      xs = vsplat<real>(xval[i]) * apply_owned_row<real, KP>(S, Pd, W, alpha, (size_t)xidx[i] * KP + li * G::VE);
+    } else if (one) {
+      xs = vsplat<real>(xval[i]) * vld<real>(S + (size_t)xidx[i] * KP + li * G::VE);
+    } else {
+      for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
+        xs += vsplat<real>(xval[p]) * vld<real>(S + (size_t)xidx[p] * KP + li * G::VE);
+    }
+    vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
+    vst<real>(XS + i * KP + li * G::VE, xs);
   }
 }
 

@@ -301,7 +301,7 @@ def test_fp32_runs_bit_identical(ds_name, monkeypatch):
 
 @pytest.mark.parametrize("env", [{"OCFFM_FUSE": "2"}, {"OCFFM_FUSE": "0"}, {"OCFFM_SEG_LEN": "3"}, {"OCFFM_LOOKAHEAD": "3"}, {"OCFFM_SCATTER": "1"},
                                  {"OCFFM_FUSE": "2", "OCFFM_SEG_LEN": "2"}, {"OCFFM_CGRAM": "0"},
-                                 {"OCFFM_NO_FOLD": "1"}])
+                                 {"OCFFM_NO_FOLD": "1"}, {"OCFFM_LAZY_BASE": "0"}])
 def test_execution_variants_fp64(kk_small, monkeypatch, env):
     """Schedule knobs (id-field row fusion, segment length, CG look-ahead)
     change the kernels that run, never the result."""

@@ -726,7 +726,9 @@ __global__ __launch_bounds__(BLOCK) void k_init_ytilde(uint64_t R, const int64_t
 // FUSE (id-like field: one node per row, each feature in exactly one row):
 // the CSC is the identity, so instead of writing h the kernel finalises the
 // row's feature column itself (col_arrive / col_finalize, MODE 0).
-template <typename real, int KP, bool MLDS, bool FUSE>
+enum { BM_FULL = 0, BM_IN = 1, BM_ENTER = 2 };  // base modes of k_gd_cross_seg
+
+template <typename real, int KP, bool MLDS, bool FUSE, int BM>
 __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                         const uint32_t *__restrict__ ycol,
                                                         real *__restrict__ yt, const real *__restrict__ Q1,
@@ -738,6 +740,7 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
                                                         const uint32_t *__restrict__ xidx,
                                                         const real *__restrict__ xval, uint64_t q1rows,
                                                         Fin<real> f, const uint32_t *__restrict__ segptr,
+                                                        const real *__restrict__ cur,
                                                         const real *__restrict__ drow,
                                                         const real *__restrict__ dxs, real *__restrict__ yt_other,
                                                         const uint32_t *__restrict__ perm) {
@@ -764,14 +767,24 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
     bQ[e] = (real)sums[KP + li * G::VE + e];
   }
   double dsum[3] = {0, 0, 0};
-  // dxs (deferred base update of the previous cross half):
-  // base_ij += <drow_i, dxs_j> is applied here, on the fly, and the new base is
-  // stored in both orientations (this one in place, the other through perm).
+  // Block-excluded y~.  During the cross loop the stored value is
+  // e_ij = y~_ij - <P_b[i], Q_b[j]> for the current cross block b: the halves'
+  // updates of P_b / Q_b leave it untouched, and the biases (constant over the
+  // cross loop) are folded in.  cur = this half's own factor of block b (its
+  // partner factor is the gathered q_j).
+  //   BM_FULL : base stored; y~ = base + a_i + b_j
+  //   BM_IN   : inside block b; y~ = e + <cur_i, q_j>
+  //   BM_ENTER: entering block b; y~ = e' + <drow_i, dxs_j> (e' of block b',
+  //             drow/dxs its factors) or base + a_i + b_j (dxs null); stores
+  //             e = y~ - <cur_i, q_j> here (and through perm with yt_other).
+  constexpr bool WR = BM == BM_ENTER;
   auto body = [&](const Seg &sgm) -> vec_t<real> {
     const uint64_t i = sgm.row;
     const real ai = a1[i];
     vec_t<real> pk = vzero<real>();
-    const vec_t<real> dr = dxs ? vld<real>(drow + i * KP + li * G::VE) : vzero<real>();
+    const vec_t<real> dr = (WR && dxs) ? vld<real>(drow + i * KP + li * G::VE) : vzero<real>();
+    const vec_t<real> cr = BM != BM_FULL ? vld<real>(cur + i * KP + li * G::VE) : vzero<real>();
+    const bool gbias = BM == BM_FULL || (WR && !dxs);
     for (int64_t p0 = sgm.b; p0 < sgm.e; p0 += PP::PW) {
       uint32_t jj[PP::UT];
       real yv[PP::UT];
@@ -781,33 +794,40 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
         const int64_t q = p0 + li + t * G::LPR;
         yv[t] = q < sgm.e ? yt[q] : (real)0;
       }
-      real yn[PP::UT];  // dxs: the new base of this lane's positions
+      real yn[PP::UT];  // WR: e of this lane's positions
 #pragma unroll
       for (int t = 0; t < PP::UT; t++) yn[t] = yv[t];
       sfor<PP::PW / PP::GB>([&](auto BT) {
         constexpr int bt = decltype(BT)::value * PP::GB;
         if (p0 + bt >= sgm.e) return;
-        vec_t<real> qv[PP::GB], xv[PP::GB];
-        real cb[PP::GB], yb[PP::GB];
+        vec_t<real> qv[PP::GB], xv[WR ? PP::GB : 1];
+        real yb[PP::GB];
         sfor<PP::GB>([&](auto U) {
           constexpr int u = decltype(U)::value;
           const uint32_t j = PP::template at<bt + u>(jj, li);
           yb[u] = PP::template at<bt + u>(yv, li);
           qv[u] = bld<real>(qb, PP::row_off(j, qb, li));
-          cb[u] = bld1<real>(bb, j == POS_NONE ? bb.oob : j * (uint32_t)sizeof(real));
-          if (dxs) xv[u] = bld<real>(xb, PP::row_off(j, xb, li));
+          if (gbias) yb[u] += ai + bld1<real>(bb, j == POS_NONE ? bb.oob : j * (uint32_t)sizeof(real));
+          if constexpr (WR) {
+            if (dxs) xv[u] = bld<real>(xb, PP::row_off(j, xb, li));
+          }
         });
-        if (dxs) {
+        if constexpr (BM != BM_FULL) {
 #pragma unroll
           for (int u = 0; u < PP::GB; u++) {
-            yb[u] += sg_sum<G::LPR>(hsum<real>(dr * xv[u]));
-            if ((bt + u) % G::LPR == li) yn[(bt + u) / G::LPR] = yb[u];
+            const real c = sg_sum<G::LPR>(hsum<real>(cr * qv[u]));
+            if constexpr (WR) {
+              if (dxs) yb[u] += sg_sum<G::LPR>(hsum<real>(dr * xv[u]));
+              if ((bt + u) % G::LPR == li) yn[(bt + u) / G::LPR] = yb[u] - c;
+            } else {
+              yb[u] += c;
+            }
           }
         }
 #pragma unroll
-        for (int u = 0; u < PP::GB; u++) pk += vsplat<real>(cpos * (yb[u] + ai + cb[u]) - cneg) * qv[u];
+        for (int u = 0; u < PP::GB; u++) pk += vsplat<real>(cpos * yb[u] - cneg) * qv[u];
       });
-      if (dxs) {
+      if constexpr (WR) {
 #pragma unroll
         for (int t = 0; t < PP::UT; t++) {
           const int64_t q = p0 + li + t * G::LPR;
@@ -819,9 +839,19 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
       }
     }
     if (seg_first(sgm)) {
+      // T_i: the C row loads are independent; issue them in batches so the
+      // vector-matrix products do not wait on one HBM round trip per table
+      constexpr int CB = 4;
       vec_t<real> t = vzero<real>();
-      for (int c = 0; c < C; c++)
-        t += sg_vecmat<real, KP>(vld<real>(Ptabs[c] + i * KP + li * G::VE), Mp + (size_t)c * KP * KP, li);
+      for (int c0 = 0; c0 < C; c0 += CB) {
+        vec_t<real> pc[CB];
+#pragma unroll
+        for (int u = 0; u < CB; u++)
+          pc[u] = c0 + u < C ? vld<real>(Ptabs[c0 + u] + i * KP + li * G::VE) : vzero<real>();
+#pragma unroll
+        for (int u = 0; u < CB; u++)
+          if (c0 + u < C) t += sg_vecmat<real, KP>(pc[u], Mp + (size_t)(c0 + u) * KP * KP, li);
+      }
       const real z = ai - (real)r;
       pk += vsplat<real>((real)w) * (t + vsplat<real>(z) * oQ + bQ);
     }
@@ -1579,7 +1609,9 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
                                                             real *__restrict__ yt_other,
                                                             const uint32_t *__restrict__ perm, real *__restrict__ W,
                                                             const real *__restrict__ Pd, const CgState *st,
-                                                            const real *__restrict__ XSin) {
+                                                            const real *__restrict__ XSin,
+                                                            const real *__restrict__ a1,
+                                                            const real *__restrict__ b1) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP>;
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real));
@@ -1590,8 +1622,10 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
     const Seg sgm = segs[s];
     const uint64_t i = sgm.row;
     vec_t<real> xs = vzero<real>();
-    if (XSin) {  // flush of a deferred base update: XS given, P already updated
+    real ai = 0;
+    if (XSin) {  // flush of the block-excluded y~ (a1/b1: its biases come out)
       xs = vld<real>(XSin + i * KP + li * G::VE);
+      ai = a1[i];
     } else if (W) {  // id-like field (segd set): the row's first segment does its feature's k_apply work
       const size_t off = (size_t)segd[s] * KP + li * G::VE;
       const vec_t<real> sf = seg_first(sgm) ? apply_owned_row<real, KP>(S, Pd, W, alpha, off)
@@ -1635,6 +1669,7 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
         const int64_t q = p0 + li + t * G::LPR;
         ym[t] = q < sgm.e ? yt[q] : (real)0;
         pm[t] = (yt_other && q < sgm.e) ? perm[q] : 0u;
+        if (XSin && q < sgm.e) ym[t] -= ai + b1[jj[t]];
       }
 #pragma unroll
       for (int t = 0; t < PP::UT; t++) {
@@ -1649,10 +1684,10 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
   }
 }
 
-// The cross update without its positive pass (deferred base update, DESIGN
-// §2): XS_i = X_i S, P_i += XS_i, and XS kept for the next cross half's
-// gradient pass, which applies base_ij += <XS_i, q_j> on the fly.  W
-// non-null (id-like field): the row also does its feature's k_apply work.
+// The cross update without its positive pass (block-excluded base, DESIGN
+// §2: the stored base does not depend on this block's factors):
+// XS_i = X_i S, P_i += XS_i (and XS_i kept when XS is given).  W non-null
+// (id-like field): the row also does its feature's k_apply work.
 template <typename real, int KP>
 __global__ __launch_bounds__(BLOCK) void k_update_cross_rows(uint64_t R, const int64_t *__restrict__ xptr,
                                                              const uint32_t *__restrict__ xidx,
@@ -1675,7 +1710,7 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_rows(uint64_t R, const i
         xs += vsplat<real>(xval[p]) * vld<real>(S + (size_t)xidx[p] * KP + li * G::VE);
     }
     vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
-    vst<real>(XS + i * KP + li * G::VE, xs);
+    if (XS) vst<real>(XS + i * KP + li * G::VE, xs);
   }
 }
 

@@ -405,7 +405,6 @@ template <typename real> class Problem final : public ProblemBase {
     if (comm_.host_fn) HIPCHK(hipHostMalloc((void **)&dstage_, DSTAGE * sizeof(double), hipHostMallocDefault));
     dots_.alloc(4);
     bsum_.alloc(2);
-    xsbuf_.alloc(std::max<uint64_t>(std::max(U_.R, V_.R), 1) * kp_);
   }
 
   ~Problem() override {
@@ -524,18 +523,20 @@ template <typename real> class Problem final : public ProblemBase {
       for (uint32_t f1 = fu_; f1 < f_; f1++)
         for (uint32_t f2 = f1; f2 < f_; f2++) solve_block(f1, f2);
     }
-    // cross blocks: each half's base update is deferred to the next cross
-    // half's gradient pass, except the last one's (the side halves of the
-    // next epoch read the base)
-    for (uint32_t f1 = 0; f1 < fu_; f1++)
-      for (uint32_t f2 = fu_; f2 < f_; f2++) {
-        const bool last = f1 + 1 == fu_ && f2 + 1 == f_;
-        lazy_ok_ = true;
-        half(f1, f2, 0);
-        lazy_ok_ = !last;
-        half(f1, f2, 1);
-        lazy_ok_ = false;
-      }
+    // cross blocks on the block-excluded base, restored after the
+    // last one (the side halves and the next epoch read the full base)
+    lazy_ok_ = lazy_base_;
+    try {
+      for (uint32_t f1 = 0; f1 < fu_; f1++)
+        for (uint32_t f2 = fu_; f2 < f_; f2++) {
+          half(f1, f2, 0);
+          half(f1, f2, 1);
+        }
+    } catch (...) {
+      lazy_ok_ = false;
+      throw;
+    }
+    lazy_ok_ = false;
     flush_base();
     if (prm_.self_side) cache_sasb();
     if (timing_) {
@@ -1343,6 +1344,7 @@ template <typename real> class Problem final : public ProblemBase {
   void gradient(HalfCtx &h) {
     DevSide<real> &own = *h.own;
     const bool fz_ = fused_rows(h, false);
+    if (!(lazy_ok_ && h.cross)) flush_base();  // this half reads (or updates) the full base
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
       using Gm = Geo<real, KP>;
@@ -1353,25 +1355,39 @@ template <typename real> class Problem final : public ProblemBase {
         aggregates(ps.R, (int)C_, partner_tabs(h), h.Q1, ps.bias.p, M_.p);  // M_c, oQ, bQ
         const size_t msz = (size_t)C_ * KP * KP * sizeof(real);
         const bool lds = msz <= 64 * 1024;
-        const double bytes = (double)own.R * 8 + (double)own.npos * (4 + rs) + (double)ps.R * KP * rs +
-                             (double)C_ * own.R * KP * rs + (double)own.R * rs + (double)own.R * KP * rs;
+        double bytes = (double)own.R * 8 + (double)own.npos * (4 + rs) + (double)ps.R * KP * rs +
+                       (double)C_ * own.R * KP * rs + (double)own.R * rs + (double)own.R * KP * rs;
         DevField<real> &F = *h.F;
         const Fin<real> fin = make_fin(h, 0);
-        // a deferred base update of the previous cross half is applied by this pass
-        const real *drow = nullptr, *dxs = nullptr;
-        if (pend_.on) {
-          if (pend_.user == h.user || fz_) throw Error(OCFFM_E_STATE, "deferred base update out of order");
-          drow = pend_.user ? Q_[pend_.b12].p : P_[pend_.b12].p;  // indexed by this half's rows
-          dxs = xsbuf_.p;                                        // indexed by the partner
-          pend_.on = false;
+        // block-excluded base: enter this block (store), or read it inside
+        const real *cur = nullptr, *drow = nullptr, *dxs = nullptr;
+        bool enter = false;
+        if (lazy_ok_) {
+          cur = h.P1;
+          enter = !(excl_.on && excl_.b12 == h.b12);
+          if (enter && excl_.on) {  // leave the previous block in the same pass
+            drow = h.user ? P_[excl_.b12].p : Q_[excl_.b12].p;  // indexed by this half's rows
+            dxs = h.user ? Q_[excl_.b12].p : P_[excl_.b12].p;   // indexed by the partner
+          }
+          excl_ = ExclBase{true, h.b12};
         }
-        auto go = [&](auto fz, auto ml) {
+        // cur / drow are rows of the C tables already counted; entering stores e
+        // and gathers the previous block's partner rows
+        if (enter) bytes += (double)own.npos * rs + (dxs ? (double)ps.R * KP * rs : 0);
+        auto go2 = [&](auto fz, auto ml, auto bm) {
           constexpr bool FZ = decltype(fz)::value, ML = decltype(ml)::value;
-          launch(k_gd_cross_seg<real, KP, ML, FZ>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, ML ? msz : 0,
+          constexpr int BM = decltype(bm)::value;
+          launch(k_gd_cross_seg<real, KP, ML, FZ, BM>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, ML ? msz : 0,
               own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
               (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, h.partner->bias.p, w_,
               r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, (uint64_t)h.partner->R, fin, (const uint32_t *)own.segptr.p,
-              drow, dxs, lazy_scatter_ ? h.partner->yt.p : (real *)nullptr, (const uint32_t *)own.perm.p);
+              cur, drow, dxs, (enter && lazy_scatter_) ? h.partner->yt.p : (real *)nullptr,
+              (const uint32_t *)own.perm.p);
+        };
+        auto go = [&](auto fz, auto ml) {
+          if (!cur) go2(fz, ml, std::integral_constant<int, BM_FULL>());
+          else if (enter) go2(fz, ml, std::integral_constant<int, BM_ENTER>());
+          else go2(fz, ml, std::integral_constant<int, BM_IN>());
         };
         prof_launch(fz_ ? "gd_cross_fused" : "gd_cross_row", bytes, [&] {
           if (fz_) {
@@ -1382,7 +1398,7 @@ template <typename real> class Problem final : public ProblemBase {
             else go(std::false_type(), std::false_type());
           }
         });
-        if (dxs && !lazy_scatter_) refresh_other(own, *h.partner);  // the other orientation of the new base
+        if (enter && !lazy_scatter_) refresh_other(own, *h.partner);  // the other orientation
         // QTQ for CG = M of this block (M_ is not rewritten before the half ends)
         const uint32_t c0 = cross_slot(std::min(h.fl, h.fo), std::max(h.fl, h.fo));
         qtq_ = M_.p + (size_t)c0 * KP * KP;
@@ -1411,27 +1427,28 @@ template <typename real> class Problem final : public ProblemBase {
   // subgroups per wave of this problem's row geometry (kernels.hpp: Geo)
   int nsg() const { return 64 / std::max<int>(1, (int)(kp_ * sizeof(real) / 16)); }
 
-  // Apply a deferred base update now: the positive pass the
-  // cross update skipped (k_update_cross_seg with the kept XS), then the
-  // refresh of the other orientation.
+  // Restore the full base from the block-excluded y~:
+  // base_ij = e_ij + <P_b[i], Q_b[j]> - a_i - b_j in the user orientation
+  // (k_update_cross_seg with XS = P_b), then the refresh of the other one.
   void flush_base() {
-    if (!pend_.on) return;
-    pend_.on = false;
-    const Block &b = blocks_[pend_.b12];
-    DevSide<real> &own = pend_.user ? U_ : V_, &other = pend_.user ? V_ : U_;
-    DevField<real> &F = *own.F[fidx(pend_.user ? b.f1 : b.f2)];
-    const real *Q1 = pend_.user ? Q_[pend_.b12].p : P_[pend_.b12].p;
+    if (!excl_.on) return;
+    excl_.on = false;
+    const Block &b = blocks_[excl_.b12];
+    DevSide<real> &own = U_, &other = V_;
+    DevField<real> &F = *own.F[fidx(b.f1)];
+    const real *P1 = P_[excl_.b12].p, *Q1 = Q_[excl_.b12].p;
     if (own.R == 0) return;
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
       using Gm = Geo<real, KP>;
       const double rs = sizeof(real);
-      prof_launch("update_cross_row", (double)own.R * KP * rs + (double)own.npos * (4 + 2 * rs) + (double)other.R * KP * rs,
+      prof_launch("flush_base", (double)own.R * (KP + 1) * rs + (double)own.npos * (4 + 2 * rs) + (double)other.R * (KP + 1) * rs,
                   [&] {
                     launch(k_update_cross_seg<real, KP>, grid_for(own.nseg, 4 * Gm::NSG), BLOCK, 0, own.nseg,
                            own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, (const real *)S_.p, (real *)nullptr, own.ycol.p,
                            own.yt.p, Q1, (uint64_t)other.R, F.segd.p, F.segx.p, (real *)nullptr, own.perm.p,
-                           (real *)nullptr, (const real *)nullptr, (const CgState *)st_.p, (const real *)xsbuf_.p);
+                           (real *)nullptr, (const real *)nullptr, (const CgState *)st_.p, P1,
+                           (const real *)U_.bias.p, (const real *)V_.bias.p);
                   });
     });
     refresh_other(own, other);
@@ -1831,15 +1848,14 @@ template <typename real> class Problem final : public ProblemBase {
       if (own.R == 0) return;
       if (h.cross) {
         DevSide<real> &other = *h.partner;
-        if (lazy_ok_ && lazy_base_ && !scatter_ && fuse_ < 2) {
-          // deferred base update: XS kept, the next cross half's gradient pass applies it
-          prof_launch("update_cross_row", (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
-                                              (double)own.R * KP * rs * 3, [&] {
+        if (excl_.on && excl_.b12 == h.b12) {
+          // block-excluded base: the base does not depend on P1, no positive pass
+          prof_launch("update_cross_rows", (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
+                                               (double)own.R * KP * rs * 2, [&] {
             launch(k_update_cross_rows<real, KP>, grid_for(own.R, 4 * Gm::NSG), BLOCK, 0, own.R, F.xptr.p, F.xidx.p,
-                   F.xval.p, (const real *)S_.p, h.P1, xsbuf_.p, F.one, Wf, (const real *)Vd_.p,
+                   F.xval.p, (const real *)S_.p, h.P1, (real *)nullptr, F.one, Wf, (const real *)Vd_.p,
                    (const CgState *)st_.p);
           });
-          pend_ = BasePending{true, h.user, h.b12};
           return;
         }
         const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
@@ -1849,7 +1865,8 @@ template <typename real> class Problem final : public ProblemBase {
           launch(k_update_cross_seg<real, KP>, grid_for(own.nseg, 4 * Gm::NSG), BLOCK, 0,
               own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, own.ycol.p, own.yt.p, h.Q1,
               (uint64_t)other.R, F.segd.p, F.segx.p, scatter_ ? other.yt.p : nullptr, own.perm.p, Wf,
-              (const real *)Vd_.p, (const CgState *)st_.p, (const real *)nullptr);
+              (const real *)Vd_.p, (const CgState *)st_.p, (const real *)nullptr, (const real *)nullptr,
+              (const real *)nullptr);
         });
         if (!scatter_) refresh_other(own, other);  // gather the other orientation instead
       } else {
@@ -1943,19 +1960,18 @@ template <typename real> class Problem final : public ProblemBase {
   std::vector<DevBuf<real>> W_, H_, P_, Q_;
   DevBuf<real> acc_, G_, S_, Vd_, Rv_, Hv_, h_, M_, wpart_;
   DevBuf<double> bsum_;  // sums of a and b (bias_sums)
-  // Deferred base update: the cross update of block b12's user
-  // (user = true) or item half left XS in xsbuf_; the next cross half's
-  // gradient pass applies base_ij += <XS, q> (flush_base() otherwise).
-  struct BasePending {
-    bool on = false, user = false;
+  // Block-excluded y~: while `on`, both orientations of the
+  // stored base hold y~ - <P_b12[i], Q_b12[j]>; the cross halves of block
+  // b12 then update P/Q without a positive pass.  flush_base() restores it.
+  struct ExclBase {
+    bool on = false;
     uint32_t b12 = 0;
-  } pend_;
-  DevBuf<real> xsbuf_;
-  bool lazy_ok_ = false;  // set by one_epoch around the halves whose successor is a cross gradient
+  } excl_;
+  bool lazy_ok_ = false;  // set by one_epoch around its cross halves
   // OCFFM_LAZY_BASE=0: every cross update applies its base change at once
   bool lazy_base_ = !std::getenv("OCFFM_LAZY_BASE") || std::atoi(std::getenv("OCFFM_LAZY_BASE")) != 0;
-  // OCFFM_LAZY_SCATTER=1: that gradient pass also stores the other orientation
-  // (scattered 4-B stores) instead of a refresh gather after it
+  // OCFFM_LAZY_SCATTER=1: the gradient pass entering a block also stores the
+  // other orientation (scattered 4-B stores) instead of a refresh gather after it
   bool lazy_scatter_ = std::getenv("OCFFM_LAZY_SCATTER") && std::atoi(std::getenv("OCFFM_LAZY_SCATTER")) != 0;
   bool want_g_ = false;  // grad(): the gradient finalisation also stores G
   const real *qtq_ = nullptr;  // this cross half's Q^T Q: a slot of M_

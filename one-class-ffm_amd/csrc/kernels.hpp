@@ -53,6 +53,9 @@ constexpr int BLOCK = 256;   // 4 waves
 #ifndef OCFFM_HS_OCC
 #define OCFFM_HS_OCC 1
 #endif
+#ifndef OCFFM_GD_GB
+#define OCFFM_GD_GB 8  // partner-row gathers per round in k_gd_cross_seg
+#endif
 #ifndef OCFFM_GD_OCC
 #define OCFFM_GD_OCC 1
 #endif
@@ -237,6 +240,53 @@ __device__ __forceinline__ vec_t<real> sg_vecmat(const vec_t<real> &x, const rea
     const real xe = sg_bcast<G::LPR, e / G::VE>(x[e % G::VE], li);
     t += vsplat<real>(xe) * vld<real>(M + (size_t)e * KP + li * G::VE);
   });
+  return t;
+}
+
+// Lane-local vector-matrix accumulation for t = x M summed over several M
+// (fp32): lane li holds rows r = li*4 + e of x, so it adds x[e] * M[r][n] for
+// ALL n into u (no cross-lane broadcast per element), column pairs in packed
+// FMAs.  Mt is M in pair-transposed order, Mt[(n/2)*2KP + 2r + n%2] = M[r][n]:
+// per column pair two conflict-free 16-B reads.  The subgroup sums u once at
+// the end with sg_reduce_scatter.
+typedef float f2v __attribute__((ext_vector_type(2)));
+template <int KP>
+__device__ __forceinline__ void lane_vecmat_acc(f2v (&u)[KP / 2], const f4v &x, const float *Mt, int li) {
+  const f2v x0 = {x[0], x[0]}, x1 = {x[1], x[1]}, x2 = {x[2], x[2]}, x3 = {x[3], x[3]};
+#pragma unroll
+  for (int q = 0; q < KP / 2; q++) {
+    const f4v a = *reinterpret_cast<const f4v *>(Mt + q * 2 * KP + li * 8);
+    const f4v b = *reinterpret_cast<const f4v *>(Mt + q * 2 * KP + li * 8 + 4);
+    f2v s = u[q];
+    s += x0 * f2v{a[0], a[1]};
+    s += x1 * f2v{a[2], a[3]};
+    s += x2 * f2v{b[0], b[1]};
+    s += x3 * f2v{b[2], b[3]};
+    u[q] = s;
+  }
+}
+__device__ __forceinline__ int mt_index(int KP, int r, int n) { return (n >> 1) * 2 * KP + 2 * r + (n & 1); }
+// Subgroup reduce-scatter of u[KP]: lane li returns sum over the LPR lanes of
+// u[li*VE .. li*VE+VE-1] (halving exchanges, highest lane bit first).
+template <typename real, int KP>
+__device__ __forceinline__ vec_t<real> sg_reduce_scatter(real (&u)[KP], int li) {
+  using G = Geo<real, KP>;
+  sfor<6>([&](auto S) {  // stages o = LPR/2, ..., 1 (S indexes the stage)
+    constexpr int o = (G::LPR >> 1) >> decltype(S)::value;
+    if constexpr (o >= 1) {
+      constexpr int H = (KP * o) / G::LPR;  // elements kept after this stage
+      const bool up = li & o;
+#pragma unroll
+      for (int m = 0; m < H; m++) {
+        const real send = up ? u[m] : u[m + H];
+        const real keep = up ? u[m + H] : u[m];
+        u[m] = keep + __shfl_xor(send, o, 64);
+      }
+    }
+  });
+  vec_t<real> t;
+#pragma unroll
+  for (int e = 0; e < G::VE; e++) t[e] = u[e];
   return t;
 }
 
@@ -745,15 +795,24 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
                                                         const real *__restrict__ dxs, real *__restrict__ yt_other,
                                                         const uint32_t *__restrict__ perm) {
   using G = Geo<real, KP>;
-  using PP = PosPass<real, KP>;
+  using PP = PosPass<real, KP, OCFFM_GD_GB>;
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real)), bb = buf_view(b1, q1rows * sizeof(real));
   const BufView xb = buf_view(dxs, dxs ? q1rows * KP * sizeof(real) : 0);
   extern __shared__ __align__(16) unsigned char smem_raw[];
   real *Ms = reinterpret_cast<real *>(smem_raw);
   const real *Mp = M;
+  // TL: T_i by lane-local accumulation over transposed M (fp32, KP <= 32)
+  constexpr bool TL = MLDS && std::is_same<real, float>::value && KP <= 32;
   if (MLDS) {
     const int tot = C * KP * KP;
-    for (int t = threadIdx.x; t < tot; t += BLOCK) Ms[t] = M[t];
+    for (int t = threadIdx.x; t < tot; t += BLOCK) {
+      if constexpr (TL) {  // pair-transposed (lane_vecmat_acc)
+        const int c = t / (KP * KP), rn = t % (KP * KP);
+        Ms[c * KP * KP + mt_index(KP, rn / KP, rn % KP)] = M[t];
+      } else {
+        Ms[t] = M[t];
+      }
+    }
     __syncthreads();
     Mp = Ms;
   }
@@ -843,6 +902,11 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
       // vector-matrix products do not wait on one HBM round trip per table
       constexpr int CB = 4;
       vec_t<real> t = vzero<real>();
+      f2v ul[TL ? KP / 2 : 1];
+      if constexpr (TL) {
+#pragma unroll
+        for (int q = 0; q < KP / 2; q++) ul[q] = f2v{0.f, 0.f};
+      }
       for (int c0 = 0; c0 < C; c0 += CB) {
         vec_t<real> pc[CB];
 #pragma unroll
@@ -850,7 +914,19 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
           pc[u] = c0 + u < C ? vld<real>(Ptabs[c0 + u] + i * KP + li * G::VE) : vzero<real>();
 #pragma unroll
         for (int u = 0; u < CB; u++)
-          if (c0 + u < C) t += sg_vecmat<real, KP>(pc[u], Mp + (size_t)(c0 + u) * KP * KP, li);
+          if (c0 + u < C) {
+            if constexpr (TL) lane_vecmat_acc<KP>(ul, pc[u], Mp + (size_t)(c0 + u) * KP * KP, li);
+            else t += sg_vecmat<real, KP>(pc[u], Mp + (size_t)(c0 + u) * KP * KP, li);
+          }
+      }
+      if constexpr (TL) {
+        real uf[KP];
+#pragma unroll
+        for (int q = 0; q < KP / 2; q++) {
+          uf[2 * q] = ul[q][0];
+          uf[2 * q + 1] = ul[q][1];
+        }
+        t = sg_reduce_scatter<real, KP>(uf, li);
       }
       const real z = ai - (real)r;
       pk += vsplat<real>((real)w) * (t + vsplat<real>(z) * oQ + bQ);

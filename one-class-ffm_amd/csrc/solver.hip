@@ -971,6 +971,14 @@ template <typename real> class Problem final : public ProblemBase {
         v2u[q] = (uint32_t)(p - pb);
       }
     V_.npos = np;
+    if (comm_.active()) {  // the counts over ALL users (item side halves' CG steps, repl())
+      std::vector<int64_t> gptr(V.m + 1, 0);
+      for (uint64_t i = 0; i < U.m; i++)
+        for (uint64_t p = U.yptr[i]; p < U.yptr[i + 1]; p++) gptr[U.ycol[p] + 1]++;
+      for (uint64_t j = 0; j < V.m; j++) gptr[j + 1] += gptr[j];
+      gvptr_.upload(gptr);
+      gn1_ = (double)U.m;
+    }
     build_segments(V_, vptr, seg_len_, nsg());
     build_heavy(V_, vptr);
     V_.yptr.upload(vptr);
@@ -1377,7 +1385,7 @@ template <typename real> class Problem final : public ProblemBase {
         auto go2 = [&](auto fz, auto ml, auto bm) {
           constexpr bool FZ = decltype(fz)::value, ML = decltype(ml)::value;
           constexpr int BM = decltype(bm)::value;
-          launch(k_gd_cross_seg<real, KP, ML, FZ, BM>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, ML ? msz : 0,
+          launch(k_gd_cross_seg<real, KP, ML, FZ, BM>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : gd_blocks_), BLOCK, ML ? msz : 0,
               own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
               (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, h.partner->bias.p, w_,
               r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, (uint64_t)h.partner->R, fin, (const uint32_t *)own.segptr.p,
@@ -1556,7 +1564,7 @@ template <typename real> class Problem final : public ProblemBase {
       const double rs = sizeof(real);
       prof_launch("col_gram", (double)F.nnz * (8 + rs + 16 + KP * rs) + (double)F.gram.bytes(), [&] {
         launch(k_col_gram<real, KP>, (unsigned)F.gchunks.n, BLOCK, 0, F.gchunks.p, F.crow.p, F.cval.p,
-               h.own->yptr.p, h.Q1, w_, (double)other.R, F.gram.p, F.gpart.p, F.cnt.p);
+               hess_cnt(h), h.Q1, w_, hess_n1(h), F.gram.p, F.gpart.p, F.cnt.p);
       });
     });
   }
@@ -1591,13 +1599,19 @@ template <typename real> class Problem final : public ProblemBase {
   // last-arriver sum when the row spans several chunks, kernels.hpp
   // chunk_finalize).
   bool fused_rows(const HalfCtx &h, bool hv) const {
-    return h.F->idlike && !comm_.active() && (fuse_ >= 2 || (fuse_ == 1 && hv && !h.cross));
+    return h.F->idlike && (!comm_.active() || (hv && repl(h))) && (fuse_ >= 2 || (fuse_ == 1 && hv && !h.cross));
   }
 
   // Several ranks, id-like field (replicated rows, e.g. items; never an owned
   // field): the side Hessian-vector row pass writes its column partials
   // straight into acc (k_hs_side_row SCAT), no CSC scatter launch.
-  bool scat_rows(const HalfCtx &h) const { return comm_.active() && h.F->idlike && !h.F->excl && !h.cross; }
+  bool scat_rows(const HalfCtx &h) const {
+    return comm_.active() && h.F->idlike && !h.F->excl && !h.cross && !repl(h);
+  }
+  // Item side half on several ranks: CG steps computed whole on every rank.
+  bool repl(const HalfCtx &h) const { return comm_.active() && !h.cross && !h.user && !h.F->excl && gvptr_.p; }
+  const int64_t *hess_cnt(const HalfCtx &h) const { return repl(h) ? gvptr_.p : h.own->yptr.p; }
+  double hess_n1(const HalfCtx &h) const { return repl(h) ? gn1_ : (double)(h.user ? V_ : U_).R; }
 
   void scatter(HalfCtx &h, int it, bool seg) {
     DevField<real> &F = *h.F;
@@ -1659,7 +1673,7 @@ template <typename real> class Problem final : public ProblemBase {
   // all-reduce, finalisation when the partial sums must meet across ranks.
   // mode 0: gradient (it = 0), mode 1: Hessian-vector of CG iteration `it`.
   void feature_pass(HalfCtx &h, int it, bool seg, bool acc_ready = false) {
-    if (!comm_.active()) {
+    if (!comm_.active() || (it > 0 && repl(h))) {
       feat_launch(h, it, seg, it == 0 ? 0 : 1);
       return;
     }
@@ -1717,7 +1731,7 @@ template <typename real> class Problem final : public ProblemBase {
         using Gm = Geo<real, KP>;
         const double rs = sizeof(real);
         const Fin<real> fin = make_fin(h, it);
-        if (!comm_.active()) {
+        if (!comm_.active() || repl(h)) {
           prof_launch("hv_cgram", (double)h.D * KP * KP * rs + (double)h.D * KP * rs * (it > 1 ? 9 : 4), [&] {
             launch(k_hv_cgram<real, KP>, grid_for(h.D, 4 * Gm::NSG, 1024), BLOCK, 0, (uint64_t)h.D,
                    (const real *)h.F->gram.p, fin);
@@ -1765,14 +1779,13 @@ template <typename real> class Problem final : public ProblemBase {
             }
           });
         } else {
-          DevSide<real> &other = h.user ? V_ : U_;
-          const double n1 = (double)other.R;
+          const double n1 = hess_n1(h);
           const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
                                (double)own.R * KP * rs * 2;
           auto go = [&](auto fz, auto sc) {
             constexpr bool FZ = decltype(fz)::value, SC = decltype(sc)::value;
             launch(k_hs_side_row<real, KP, FZ, SC>, grid_for(own.R, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, 0,
-                own.R, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.yptr.p, h.Q1, w_, n1, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
+                own.R, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, hess_cnt(h), h.Q1, w_, n1, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
                 F.one, fin);
           };
           prof_launch(fz_ ? "hs_side_fused" : "hs_side_row", bytes, [&] {
@@ -1915,6 +1928,12 @@ template <typename real> class Problem final : public ProblemBase {
   // ------------------------------------------------------------- state
   ocffm_param prm_;
   Comm comm_;
+  // Several ranks: per-item positive counts and the user count over all
+  // ranks.  An item side half's Hessian is a function of these and of the
+  // replicated item tables only, so its CG steps run on every rank in full
+  // with no all-reduce (repl()); its gradient is still a sum over users.
+  DevBuf<int64_t> gvptr_;
+  double gn1_ = 0;
   bool has_test_;
   bool inited_ = false;
   hipStream_t stream_ = nullptr;
@@ -1973,6 +1992,8 @@ template <typename real> class Problem final : public ProblemBase {
   // OCFFM_LAZY_SCATTER=1: the gradient pass entering a block also stores the
   // other orientation (scattered 4-B stores) instead of a refresh gather after it
   bool lazy_scatter_ = std::getenv("OCFFM_LAZY_SCATTER") && std::atoi(std::getenv("OCFFM_LAZY_SCATTER")) != 0;
+  // grid cap of the cross gradient pass (each block stages the C aggregates M in LDS)
+  unsigned gd_blocks_ = std::getenv("OCFFM_GD_BLOCKS") ? (unsigned)std::atoi(std::getenv("OCFFM_GD_BLOCKS")) : 2048u;
   bool want_g_ = false;  // grad(): the gradient finalisation also stores G
   const real *qtq_ = nullptr;  // this cross half's Q^T Q: a slot of M_
   DevBuf<unsigned> tick_;

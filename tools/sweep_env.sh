@@ -8,6 +8,6 @@ vals=$2
 steps=${3:-10}
 mkdir -p gpurun_out
 for v in $vals; do
-  env $var=$v timeout -k 10 300 python bench.py --steps $steps --warmup 2 --cpu-baseline off --sgd off > gpurun_out/sweep_${var}_$v.json 2> gpurun_out/sweep_${var}_$v.err
-  python -c "import json,sys; d=json.loads(open('gpurun_out/sweep_${var}_$v.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$var=$v', d['ms_per_step'], 'ms/step', r['kernel'], r['avg_launch_us'], 'us', 'frac', r['frac'])"
+  env $var=$v timeout -k 10 300 python bench.py --steps $steps --warmup 2 --cpu-baseline off --sgd off > gpurun_out/sweep_${var}_$(basename $v).json 2> gpurun_out/sweep_${var}_$(basename $v).err
+  python -c "import json,sys; d=json.loads(open('gpurun_out/sweep_${var}_$(basename $v).json').read().strip().splitlines()[-1]); r=d['roofline']; print('$var=$v', d['ms_per_step'], 'ms/step', r['kernel'], r['avg_launch_us'], 'us', 'frac', r['frac'])"
 done

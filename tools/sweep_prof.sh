@@ -9,7 +9,7 @@ fams=$3
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 for v in $vals; do
-  d=gpurun_out/sp_${var}_$v
+  d=gpurun_out/sp_${var}_$(basename $v)
   rm -rf $d
   env $var=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $d -o run -- \
     python bench.py --steps 10 --warmup 2 --cpu-baseline off --sgd off > $d.json 2> $d.err

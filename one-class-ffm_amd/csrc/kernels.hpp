@@ -1967,47 +1967,61 @@ __global__ __launch_bounds__(BLOCK) void k_gram_part(uint64_t Rp, int L, const r
 // m = 8(r/4) + 4(l/32) + r%4, n = l%32.  The four waves of a block take
 // interleaved row pairs and are combined in wave order through LDS
 // (deterministic).  Column sums ride along on the B operand.
-template <int LMAX>
-__global__ __launch_bounds__(BLOCK) void k_gram_mfma32(uint64_t Rp, int L, const float *const *__restrict__ A,
+template <int L>
+__global__ __launch_bounds__(BLOCK) void k_gram_mfma32(uint64_t Rp, const float *const *__restrict__ A,
                                                       const float *__restrict__ B, const float *__restrict__ wv,
                                                       double *__restrict__ part, uint64_t rows_per_block) {
   typedef float f16x __attribute__((ext_vector_type(16)));
   constexpr int U = 4;  // row pairs per wave per round
-  __shared__ float red[LMAX][1024];
+  __shared__ float red[L][1024];
   __shared__ float redc[3][32];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int e = lane & 31, hf = lane >> 5;
-  f16x acc[LMAX];
+  f16x acc[L];
 #pragma unroll
-  for (int c = 0; c < LMAX; c++)
+  for (int c = 0; c < L; c++)
 #pragma unroll
     for (int r = 0; r < 16; r++) acc[c][r] = 0.0f;
-  const float *Ap[LMAX];
+  // raw buffer loads (a table pointer read from memory would make the
+  // compiler fall back to flat loads); rows past the end read zero
+  BufView ab[L];
 #pragma unroll
-  for (int c = 0; c < LMAX; c++) Ap[c] = c < L ? A[c] : nullptr;
+  for (int c = 0; c < L; c++) ab[c] = buf_view(A[c], Rp * 128);
+  const BufView bb = buf_view(B, B ? Rp * 128 : 0), wb = buf_view(wv, wv ? Rp * 4 : 0);
   float cs = 0, ws = 0, wt = 0;
   const uint64_t r0 = (uint64_t)blockIdx.x * rows_per_block;
   const uint64_t r1 = min(Rp, r0 + rows_per_block);
-  for (uint64_t j0 = r0 + 2 * w; j0 < r1; j0 += 8 * U) {
-    float bv[U], wvv[U], av[U][LMAX];
+  // two register sets: the next round's loads are in flight while this
+  // round's MFMAs run (one wave per SIMD: the loop is latency-bound)
+  float bv[2][U], wvv[2][U], av[2][U][L];
+  auto load = [&](int sb, uint64_t j0) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint64_t jj = j0 + 8 * u + hf;
       const bool ok = jj < r1;
-      bv[u] = (ok && B) ? B[jj * 32 + e] : 0.0f;
-      wvv[u] = (ok && wv) ? wv[jj] : 0.0f;
+      const uint32_t off = ok ? (uint32_t)(jj * 128 + e * 4) : 0xffffffffu;
+      bv[sb][u] = bld1<float>(bb, off);
+      wvv[sb][u] = bld1<float>(wb, ok ? (uint32_t)(jj * 4) : 0xffffffffu);
 #pragma unroll
-      for (int c = 0; c < LMAX; c++) av[u][c] = (ok && c < L) ? Ap[c][jj * 32 + e] : 0.0f;
+      for (int c = 0; c < L; c++) av[sb][u][c] = bld1<float>(ab[c], off);
     }
+  };
+  auto step = [&](int sb) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
 #pragma unroll
-      for (int c = 0; c < LMAX; c++)
-        if (c < L) acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u][c], bv[u], acc[c], 0, 0, 0);
-      cs += bv[u];
-      ws += wvv[u] * bv[u];
-      if (e == 0) wt += wvv[u];
+      for (int c = 0; c < L; c++) acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[sb][u][c], bv[sb][u], acc[c], 0, 0, 0);
+      cs += bv[sb][u];
+      ws += wvv[sb][u] * bv[sb][u];
+      if (e == 0) wt += wvv[sb][u];
     }
+  };
+  // rows past r1 load zeros (buffer range check), so a trailing round is harmless
+  for (uint64_t j0 = r0 + 2 * w; j0 < r1; j0 += 16 * U) {
+    load(0, j0);
+    load(1, j0 + 8 * U);
+    step(0);
+    step(1);
   }
   // column sums: the two half-waves hold even / odd rows of the same column
   cs += __shfl_xor(cs, 32, 64);
@@ -2016,8 +2030,7 @@ __global__ __launch_bounds__(BLOCK) void k_gram_mfma32(uint64_t Rp, int L, const
   for (int ww = 0; ww < BLOCK / 64; ww++) {
     if (w == ww) {
 #pragma unroll
-      for (int c = 0; c < LMAX; c++)
-        if (c < L)
+      for (int c = 0; c < L; c++)
 #pragma unroll
           for (int r = 0; r < 16; r++) {
             const int m = 8 * (r >> 2) + 4 * hf + (r & 3);

@@ -1184,20 +1184,22 @@ template <typename real> class Problem final : public ProblemBase {
     const size_t rs = sizeof(real);
     const int TR = kp_ >= 64 ? 16 : 32;
     // tables per launch so the LDS stage fits in 64 KB (MFMA path: its register budget)
-    const int lmax = mfma_gram(L) ? GRAM_LMAX
+    const bool mg = mfma_gram(L) && (uint64_t)Rp * 128 < 0xffffff00ull;  // buffer-load offsets are 32-bit
+    const int lmax = mg ? GRAM_LMAX
                                   : std::max<int>(1, (int)((64 * 1024 / rs - (size_t)TR * kp_ - TR) / ((size_t)TR * kp_)));
     int l0 = 0;
     bool first = true;
     do {
       const int Lc = std::min(L - l0, lmax);
       launch_aggr(Rp, Lc, A ? A + l0 : nullptr, B, first ? wv : nullptr, M ? M + (size_t)l0 * kp_ * kp_ : nullptr,
-                  first);
+                  first, mg);
       l0 += Lc;
       first = false;
     } while (l0 < L);
   }
 
-  void launch_aggr(uint64_t Rp, int L, const real *const *A, const real *B, const real *wv, real *M, bool sums) {
+  void launch_aggr(uint64_t Rp, int L, const real *const *A, const real *B, const real *wv, real *M, bool sums,
+                   bool mg) {
     const int TR = kp_ >= 64 ? 16 : 32;
     const size_t smem = ((size_t)L * TR * kp_ + (size_t)TR * kp_ + TR) * sizeof(real);
     const uint64_t nout = (uint64_t)L * kp_ * kp_ + 2 * kp_ + 1;
@@ -1211,13 +1213,25 @@ template <typename real> class Problem final : public ProblemBase {
       nbx = std::min<uint64_t>(nbx, std::max<uint64_t>(1, part_.n / nout));
       const uint64_t rpb = (Rp + nbx - 1) / nbx;
       const double abytes = (double)Rp * ((L + (B ? 1 : 0)) * kp_ + (wv ? 1 : 0)) * sizeof(real);
-      if (mfma_gram(L)) {  // fp32, KP = 32: the Grams on MFMA (kernels.hpp k_gram_mfma32)
+      if (mg) {  // fp32, KP = 32: the Grams on MFMA (kernels.hpp k_gram_mfma32)
         nbx = std::max<uint64_t>(1, std::min<uint64_t>((Rp + 127) / 128, gram_blocks_));
         nbx = std::min<uint64_t>(nbx, std::max<uint64_t>(1, part_.n / nout));
         const uint64_t rpbm = (Rp + nbx - 1) / nbx;
         prof_launch("aggregates", abytes, [&] {
-          launch(k_gram_mfma32<GRAM_LMAX>, (unsigned)nbx, BLOCK, 0, Rp, L, (const float *const *)A, (const float *)B,
-                 (const float *)wv, part_.p, rpbm);
+          auto go = [&](auto lc) {
+            launch(k_gram_mfma32<decltype(lc)::value>, (unsigned)nbx, BLOCK, 0, Rp, (const float *const *)A,
+                   (const float *)B, (const float *)wv, part_.p, rpbm);
+          };
+          switch (L) {  // the table count is a compile-time constant of the kernel
+            case 1: go(std::integral_constant<int, 1>()); break;
+            case 2: go(std::integral_constant<int, 2>()); break;
+            case 3: go(std::integral_constant<int, 3>()); break;
+            case 4: go(std::integral_constant<int, 4>()); break;
+            case 5: go(std::integral_constant<int, 5>()); break;
+            case 6: go(std::integral_constant<int, 6>()); break;
+            case 7: go(std::integral_constant<int, 7>()); break;
+            default: go(std::integral_constant<int, GRAM_LMAX>()); break;
+          }
         });
       } else {
         prof_launch("aggregates", abytes, [&] {
@@ -1967,7 +1981,7 @@ template <typename real> class Problem final : public ProblemBase {
   // more than the coalesced gather pass)
   bool scatter_ = std::getenv("OCFFM_SCATTER") != nullptr;
   bool no_mfma_ = std::getenv("OCFFM_NO_MFMA") != nullptr;  // Grams on the VALU kernel instead
-  uint64_t gram_blocks_ = std::getenv("OCFFM_GRAM_BLOCKS") ? std::strtoull(std::getenv("OCFFM_GRAM_BLOCKS"), nullptr, 10) : 256;
+  uint64_t gram_blocks_ = std::getenv("OCFFM_GRAM_BLOCKS") ? std::strtoull(std::getenv("OCFFM_GRAM_BLOCKS"), nullptr, 10) : 512;
   bool no_owned_ = false;
   bool owned_stale_ = false;  // owned tables differ across ranks until sync_owned()
   unsigned hs_blocks_ = 4096;  // grid cap of the cross Hessian-vector row pass

@@ -103,6 +103,13 @@ struct CgState {
 template <typename real> __device__ __forceinline__ vec_t<real> vld(const real *p) {
   return *reinterpret_cast<const vec_t<real> *>(p);
 }
+// The same through a pointer that was itself read from memory (a table of
+// tables): the cast to the global address space keeps the load a global_load
+// (a flat load would make every wait also drain the LDS counter).
+template <typename real> __device__ __forceinline__ vec_t<real> gvld(const real *p) {
+  typedef const __attribute__((address_space(1))) vec_t<real> gvec;
+  return *(gvec *)p;
+}
 // Stores of pass outputs.  OCFFM_NT_STORES=1 at build time makes them
 // non-temporal (global_store ... nt): the bytes stream out instead of
 // sitting dirty in the XCD's L2 until the kernel-end write-back, which the
@@ -719,7 +726,7 @@ __global__ __launch_bounds__(BLOCK) void k_rowdot_multi(uint64_t R, int C, const
   for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
     real s = 0;
     for (int c = 0; c < C; c++) {
-      const vec_t<real> t = vld<real>(tabs[c] + i * KP + li * G::VE);
+      const vec_t<real> t = gvld<real>(tabs[c] + i * KP + li * G::VE);
       vec_t<real> v;
 #pragma unroll
       for (int e = 0; e < G::VE; e++) v[e] = (real)vecs[(size_t)c * KP + li * G::VE + e];
@@ -751,7 +758,7 @@ __global__ __launch_bounds__(BLOCK) void k_init_ytilde(uint64_t R, const int64_t
       const uint32_t j = ycol[p];
       real s = 0;
       for (int c = 0; c < C; c++)
-        s += sg_sum<G::LPR>(hsum<real>(vld<real>(Ptabs[c] + i * KP + li * G::VE) *
+        s += sg_sum<G::LPR>(hsum<real>(gvld<real>(Ptabs[c] + i * KP + li * G::VE) *
                                        vld<real>(Qtabs[c] + (size_t)j * KP + li * G::VE)));
       if (li == 0) {
         const real v = s - (real)1;  // base_ij; y~_ij = base_ij + a_i + b_j
@@ -911,7 +918,7 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
         vec_t<real> pc[CB];
 #pragma unroll
         for (int u = 0; u < CB; u++)
-          pc[u] = c0 + u < C ? vld<real>(Ptabs[c0 + u] + i * KP + li * G::VE) : vzero<real>();
+          pc[u] = c0 + u < C ? gvld<real>(Ptabs[c0 + u] + i * KP + li * G::VE) : vzero<real>();
 #pragma unroll
         for (int u = 0; u < CB; u++)
           if (c0 + u < C) {

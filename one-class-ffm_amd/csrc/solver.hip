@@ -47,7 +47,15 @@ static uint32_t pad_k(uint32_t k) {
   return kp;
 }
 
+// OCFFM_EXP_KP32 (experiment builds only, tools/build_variant.sh): fp32 at
+// KP = 32 instantiated alone, so a kernel experiment compiles in a fraction
+// of the full build's time.
 template <class F> static void with_kp(uint32_t kp, F &&f) {
+#ifdef OCFFM_EXP_KP32
+  if (kp != 32) throw Error(OCFFM_E_ARG, "experiment build: k must pad to 32");
+  f(std::integral_constant<int, 32>());
+  return;
+#endif
   switch (kp) {
     case 4: f(std::integral_constant<int, 4>()); break;
     case 8: f(std::integral_constant<int, 8>()); break;
@@ -2155,8 +2163,10 @@ static int create_impl(const ocffm_data *U, const ocffm_data *Ut, const ocffm_da
     const HostData *ut = Ut ? &Ut->d : nullptr;
     if (p->precision == OCFFM_FP32)
       pr->p = std::make_unique<Problem<float>>(U->d, ut, V->d, *p, comm);
+#ifndef OCFFM_EXP_KP32
     else if (p->precision == OCFFM_FP64)
       pr->p = std::make_unique<Problem<double>>(U->d, ut, V->d, *p, comm);
+#endif
     else
       throw Error(OCFFM_E_ARG, "precision must be 32 or 64");
     *out = pr.release();

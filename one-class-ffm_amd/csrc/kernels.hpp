@@ -1642,7 +1642,9 @@ __global__ __launch_bounds__(BLOCK) void k_fin(uint64_t nv, Fin<real> f) {
 template <typename real>
 __global__ __launch_bounds__(BLOCK) void k_apply(uint64_t nv, const real *__restrict__ P, real *__restrict__ S,
                                                  real *__restrict__ W, const CgState *st,
-                                                 const uint8_t *__restrict__ own, uint32_t lpr) {
+                                                 const uint8_t *__restrict__ own, uint32_t lpr,
+                                                 const int *__restrict__ skip) {
+  if (skip && *skip) return;  // speculative update of a CG solve that went on (solver.hip finish_half)
   const real alpha = st->nr_cg >= 1 ? (real)st->alpha : (real)0;
   VEC_LOOP {
     if (own && !own[v / lpr]) continue;
@@ -1694,9 +1696,11 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
                                                             const real *__restrict__ Pd, const CgState *st,
                                                             const real *__restrict__ XSin,
                                                             const real *__restrict__ a1,
-                                                            const real *__restrict__ b1) {
+                                                            const real *__restrict__ b1,
+                                                            const int *__restrict__ skip) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP>;
+  if (skip && *skip) return;
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real));
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
@@ -1777,8 +1781,10 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_rows(uint64_t R, const i
                                                              const real *__restrict__ xval,
                                                              const real *__restrict__ S, real *__restrict__ P1,
                                                              real *__restrict__ XS, bool one, real *__restrict__ W,
-                                                             const real *__restrict__ Pd, const CgState *st) {
+                                                             const real *__restrict__ Pd, const CgState *st,
+                                                             const int *__restrict__ skip) {
   using G = Geo<real, KP>;
+  if (skip && *skip) return;
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
   const real alpha = (W && st->nr_cg >= 1) ? (real)st->alpha : (real)0;
@@ -1802,7 +1808,9 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_rows(uint64_t R, const i
 // four gathers, one wide store.
 template <typename real>
 __global__ __launch_bounds__(BLOCK) void k_gather_pos(uint64_t n, const uint32_t *__restrict__ idx,
-                                                      const real *__restrict__ src, real *__restrict__ dst) {
+                                                      const real *__restrict__ src, real *__restrict__ dst,
+                                                      const int *__restrict__ skip) {
+  if (skip && *skip) return;
   for (uint64_t q = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) * 4; q < n; q += (uint64_t)gridDim.x * BLOCK * 4) {
     if (q + 4 <= n) {
       const uint4 ix = *reinterpret_cast<const uint4 *>(idx + q);
@@ -1831,8 +1839,10 @@ __global__ __launch_bounds__(BLOCK) void k_update_side_row(uint64_t R, const int
                                                            real *__restrict__ P1, const real *__restrict__ Q1,
                                                            real *__restrict__ a1, bool one, real *__restrict__ W,
                                                            const real *__restrict__ Pd, const CgState *st,
-                                                           double *__restrict__ asum, double *part, unsigned *tick) {
+                                                           double *__restrict__ asum, double *part, unsigned *tick,
+                                                           const int *__restrict__ skip) {
   using G = Geo<real, KP>;
+  if (skip && *skip) return;  // (every block: the last_block tickets stay untouched)
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
   const real alpha = (W && st->nr_cg >= 1) ? (real)st->alpha : (real)0;

@@ -1096,7 +1096,7 @@ template <typename real> class Problem final : public ProblemBase {
       HIPCHK(hipEventRecord(arm_a_, stream_));
       HIPCHK(hipEventRecord(arm_b_, stream_));
     }
-    pending_.push_back({name, bytes, arm_a_, arm_b_});
+    pending_.push_back({name, bytes, arm_a_, arm_b_, prof_tag_});
     arm_a_ = arm_b_ = nullptr;
     arm_first_ = false;
   }
@@ -1478,18 +1478,18 @@ template <typename real> class Problem final : public ProblemBase {
                            own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, (const real *)S_.p, (real *)nullptr, own.ycol.p,
                            own.yt.p, Q1, (uint64_t)other.R, F.segd.p, F.segx.p, (real *)nullptr, own.perm.p,
                            (real *)nullptr, (const real *)nullptr, (const CgState *)st_.p, P1,
-                           (const real *)U_.bias.p, (const real *)V_.bias.p);
+                           (const real *)U_.bias.p, (const real *)V_.bias.p, (const int *)nullptr);
                   });
     });
     refresh_other(own, other);
   }
 
   // other.yt (base in the other orientation) := own.yt through other.perm.
-  void refresh_other(DevSide<real> &own, DevSide<real> &other) {
+  void refresh_other(DevSide<real> &own, DevSide<real> &other, const int *skip = nullptr) {
     if (!other.npos) return;
     prof_launch("refresh_base", (double)other.npos * (4 + 2 * sizeof(real)), [&] {
       launch(k_gather_pos<real>, grid_for((other.npos + 3) / 4, BLOCK, 4096), BLOCK, 0, (uint64_t)other.npos,
-             other.perm.p, own.yt.p, other.yt.p);
+             other.perm.p, own.yt.p, other.yt.p, skip);
     });
   }
 
@@ -1855,13 +1855,62 @@ template <typename real> class Problem final : public ProblemBase {
         known = q;
       }
     };
+    // Speculative update (look-ahead 1): a half's CG count is
+    // nearly always that of the same half in the previous epoch.  At that
+    // iteration the update is queued in place of the next (usually no-op)
+    // CG step, guarded on the device by run[pred+1]: it runs only if the
+    // solve stopped by then, and returns at entry if the solve went on (the
+    // host then sees the verdict and carries on with the CG loop).  A hit
+    // saves the trailing no-op row pass + feature pass (~9 us per half).
+    // The verdicts are global, so on several ranks every rank predicts and
+    // queues the same sequence (the update itself has no collective).
+    const size_t key = (size_t)h.b12 * 2 + (size_t)which;
+    const int pred = !spec_on_ || lookahead_ != 1 ? 0
+                     : spec_fixed_ > 0          ? spec_fixed_
+                     : key < pred_.size()       ? pred_[key]
+                                                : 0;
+    bool queued = false;
+    const size_t pend0 = pending_.size();
     for (int it = 1; it <= MAXCG && !done; it++) {
+      prof_tag_ = it;
       hv_pass(h, it);
+      prof_tag_ = 0;
       const int t = it - lookahead_;
       if (t >= 1) examine(t + 1);  // upd(t) decided run[t+1]
+      if (!done && it == pred && it < MAXCG) {
+        prof_tag_ = -1;
+        finish_half(h, &st_.p->run[it + 1]);
+        prof_tag_ = 0;
+        examine(it + 1);
+        queued = done;  // stopped by iteration pred: the guarded update is the one that runs
+      }
     }
     if (!done) examine(MAXCG);
-    // apply + update
+    if (!queued) finish_half(h, nullptr);
+    if (key >= pred_.size()) pred_.resize(key + 1, 0);
+    pred_[key] = nr;
+    // profiling: launches that returned at entry (CG steps past the exit, a
+    // speculative update of a solve that went on) move no bytes; they are
+    // kept apart under "<family>.noop" so a family's rate counts real work
+    for (size_t q = pend0; q < pending_.size(); q++) {
+      Pending &e = pending_[q];
+      if (e.tag > nr || (e.tag == -1 && !queued)) e.name += ".noop";
+    }
+    cg_log.push_back(nr);
+    account_half(h, nr);
+    if (hb) {
+      hipEvent_t he = ev();
+      HIPCHK(hipEventRecord(he, stream_));
+      char name[32];
+      std::snprintf(name, sizeof(name), "half(%u,%u)%c", f1, f2, which ? 'H' : 'W');
+      pending_.push_back({name, 0.0, hb, he, 0});
+    }
+  }
+
+  // The end of a half: apply S (W += S, the last pending S += alpha p) and
+  // update P, the biases and y~ (ffm.cpp:826-832, 843-849).  skip non-null:
+  // a speculative update, whose kernels return at entry when *skip is set.
+  void finish_half(HalfCtx &h, const int *skip) {
     DevSide<real> &own = *h.own;
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
@@ -1878,7 +1927,7 @@ template <typename real> class Problem final : public ProblemBase {
       if (!fold)
         prof_launch("apply_step", (double)h.D * KP * rs * 5, [&] {
           launch(k_apply<real>, grid_for(nv, BLOCK, 2048), BLOCK, 0, nv, Vd_.p, S_.p, h.W1, st_.p,
-                 excl ? (const uint8_t *)h.F->own.p : nullptr, (uint32_t)Gm::LPR);
+                 excl ? (const uint8_t *)h.F->own.p : nullptr, (uint32_t)Gm::LPR, skip);
         });
       if (own.R == 0) return;
       if (h.cross) {
@@ -1889,7 +1938,7 @@ template <typename real> class Problem final : public ProblemBase {
                                                (double)own.R * KP * rs * 2, [&] {
             launch(k_update_cross_rows<real, KP>, grid_for(own.R, 4 * Gm::NSG), BLOCK, 0, own.R, F.xptr.p, F.xidx.p,
                    F.xval.p, (const real *)S_.p, h.P1, (real *)nullptr, F.one, Wf, (const real *)Vd_.p,
-                   (const CgState *)st_.p);
+                   (const CgState *)st_.p, skip);
           });
           return;
         }
@@ -1901,9 +1950,9 @@ template <typename real> class Problem final : public ProblemBase {
               own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, own.ycol.p, own.yt.p, h.Q1,
               (uint64_t)other.R, F.segd.p, F.segx.p, scatter_ ? other.yt.p : nullptr, own.perm.p, Wf,
               (const real *)Vd_.p, (const CgState *)st_.p, (const real *)nullptr, (const real *)nullptr,
-              (const real *)nullptr);
+              (const real *)nullptr, skip);
         });
-        if (!scatter_) refresh_other(own, other);  // gather the other orientation instead
+        if (!scatter_) refresh_other(own, other, skip);  // gather the other orientation instead
       } else {
         DevSide<real> &other = h.user ? V_ : U_;
         const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
@@ -1911,19 +1960,10 @@ template <typename real> class Problem final : public ProblemBase {
         prof_launch("update_side_row", bytes, [&] {
           launch(k_update_side_row<real, KP>, grid_for(own.R, 4 * Gm::NSG), BLOCK, 0,
               own.R, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, h.Q1, own.bias.p, F.one, Wf,
-              (const real *)Vd_.p, (const CgState *)st_.p, bsum_.p + (h.user ? 0 : 1), part_.p, tick_.p);
+              (const real *)Vd_.p, (const CgState *)st_.p, bsum_.p + (h.user ? 0 : 1), part_.p, tick_.p, skip);
         });
       }
     });
-    cg_log.push_back(nr);
-    account_half(h, nr);
-    if (hb) {
-      hipEvent_t he = ev();
-      HIPCHK(hipEventRecord(he, stream_));
-      char name[32];
-      std::snprintf(name, sizeof(name), "half(%u,%u)%c", f1, f2, which ? 'H' : 'W');
-      pending_.push_back({name, 0.0, hb, he});
-    }
   }
 
   // Algorithmic bytes of one half (SURVEY §8d formula, s = sizeof(real)).
@@ -1964,6 +2004,11 @@ template <typename real> class Problem final : public ProblemBase {
   uint64_t m_glob_ = 0, n_ = 0, u0_ = 0, u1_ = 0, dmax_ = 0, npop_ = 0;
   uint64_t seg_len_ = 32;
   int lookahead_ = 1;
+  // speculative update at the previous epoch's CG count (OCFFM_SPEC=0: off)
+  bool spec_on_ = !std::getenv("OCFFM_SPEC") || std::atoi(std::getenv("OCFFM_SPEC")) != 0;
+  std::vector<int> pred_;  // per (block, half): CG count of the last solve
+  // OCFFM_SPEC_FIXED=n (tests): predict n for every half (hits and misses of every kind)
+  int spec_fixed_ = std::getenv("OCFFM_SPEC_FIXED") ? std::atoi(std::getenv("OCFFM_SPEC_FIXED")) : 0;
   int fuse_ = 1;
   // OCFFM_RC=1: row-complete id-field cross halves (k_hs_cross_rc).  Correct
   // (tests) but measured slower at kkbox shape: 57 us per CG step against
@@ -2032,7 +2077,9 @@ template <typename real> class Problem final : public ProblemBase {
     std::string name;
     double bytes;
     hipEvent_t a, b;
+    int tag;  // CG iteration of a Hessian-vector launch, -1 a speculative update, 0 other
   };
+  int prof_tag_ = 0;
   std::vector<Pending> pending_;
   std::vector<hipEvent_t> ev_pool_, ev_free_;
 };

@@ -299,9 +299,40 @@ def test_fp32_runs_bit_identical(ds_name, monkeypatch):
     np.testing.assert_array_equal(runs[0][1], runs[1][1])
 
 
+def test_speculative_update_bit_identical(monkeypatch):
+    """The speculative end-of-half update (solver.hip half(): queued at the
+    predicted CG count, guarded on the device by the next verdict) changes
+    which kernels return at entry, never the result: predictions from the
+    previous epoch, none, and fixed ones that hit, stop early and run past
+    give bit-identical fp32 tables and CG logs over three epochs."""
+    ds = synth.kkbox(m=3000, n=4000, mean=20.0, seed=11, name="kk_det")
+    runs = {}
+    for cfg in ({"OCFFM_SPEC": "0"}, {}, {"OCFFM_SPEC_FIXED": "1"}, {"OCFFM_SPEC_FIXED": "2"},
+                {"OCFFM_SPEC_FIXED": "4"}):
+        monkeypatch.delenv("OCFFM_SPEC", raising=False)
+        monkeypatch.delenv("OCFFM_SPEC_FIXED", raising=False)
+        for k, v in cfg.items():
+            monkeypatch.setenv(k, v)
+        g = ocffm.problem_from_dataset(ds, precision=ocffm.FP32, with_test=False)
+        ocffm.srand(1)
+        g.init()
+        for _ in range(3):
+            g.one_epoch()
+        o = O.Oracle(ds, with_test=False)  # only for the block list
+        runs[str(cfg)] = ([g.get(w, b) for b in state_names(o) for w in "WH"], g.cg_log().copy())
+        g.close()
+    ref = runs[str({"OCFFM_SPEC": "0"})]
+    assert len(set(ref[1].tolist())) > 1  # the fixed predictions hit and miss
+    for name, (tabs, cg) in runs.items():
+        np.testing.assert_array_equal(cg, ref[1], err_msg=name)
+        for a, b in zip(tabs, ref[0]):
+            np.testing.assert_array_equal(a, b, err_msg=name)
+
+
 @pytest.mark.parametrize("env", [{"OCFFM_FUSE": "2"}, {"OCFFM_FUSE": "0"}, {"OCFFM_SEG_LEN": "3"}, {"OCFFM_LOOKAHEAD": "3"}, {"OCFFM_SCATTER": "1"},
                                  {"OCFFM_FUSE": "2", "OCFFM_SEG_LEN": "2"}, {"OCFFM_CGRAM": "0"},
-                                 {"OCFFM_NO_FOLD": "1"}, {"OCFFM_LAZY_BASE": "0"}])
+                                 {"OCFFM_NO_FOLD": "1"}, {"OCFFM_LAZY_BASE": "0"},
+                                 {"OCFFM_SPEC_FIXED": "1"}, {"OCFFM_SPEC_FIXED": "2"}, {"OCFFM_SPEC": "0"}])
 def test_execution_variants_fp64(kk_small, monkeypatch, env):
     """Schedule knobs (id-field row fusion, segment length, CG look-ahead)
     change the kernels that run, never the result."""

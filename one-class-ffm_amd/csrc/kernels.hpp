@@ -1204,6 +1204,79 @@ __global__ __launch_bounds__(BLOCK) void k_col_gram(const Job *__restrict__ chun
   if (threadIdx.x == 0) __hip_atomic_store(cnt + jb.col, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Per-column Grams on MFMA (fp32, KP = 32; the default where it applies).
+// One WAVE per chunk of <= CGRAM32_ROWS rows of a column: lane l stages row
+// l's index and weight c_l = d_i x_i^2, then each v_mfma_f32_32x32x2f32 takes
+// a row pair r = 2s + l/32 (A lane l = c_r q_r[l%32], B lane l = q_r[l%32],
+// the k_gram_mfma32 operand layout): the chunk's sum_r c_r q_r q_r^T builds
+// up in 16 accumulator registers with no LDS.  Every q-row load of the
+// chunk is issued before the first MFMA (one latency round).  A one-chunk
+// column stores G_c; the chunks of a longer column store their partial
+// slot (plain stores) and k_gram_slot_sum adds the slots in slot order after
+// the launch (deterministic; no tickets, no in-kernel hand-off).  Replaces
+// k_col_gram's one block per <= 128-row chunk, whose rank-1 updates read two
+// LDS words per multiply-add (genre: 32.7 us, artist: 35.4 us per build).
+constexpr int CGRAM32_ROWS = 64;
+static __global__ __launch_bounds__(BLOCK) void k_col_gram32(uint64_t nchunks, const Job *__restrict__ chunks,
+                                                      const uint32_t *__restrict__ crow,
+                                                      const float *__restrict__ cval, const int64_t *__restrict__ yptr,
+                                                      const float *__restrict__ Q1, uint64_t q1rows, double w, double n1,
+                                                      float *__restrict__ G, float *__restrict__ gpart) {
+  typedef float f16x __attribute__((ext_vector_type(16)));
+  const int lane = threadIdx.x & 63;
+  const uint64_t wv = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+  if (wv >= nchunks) return;
+  const Job jb = chunks[wv];
+  const int n = (int)(jb.e - jb.b);  // <= CGRAM32_ROWS (host)
+  uint32_t il = 0;
+  float cl = 0.0f;
+  if (lane < n) {
+    il = crow[jb.b + lane];
+    const float x = cval[jb.b + lane];
+    cl = (float)((1 - w) * (double)(yptr[il + 1] - yptr[il]) + w * n1) * x * x;
+  }
+  const BufView qb = buf_view(Q1, q1rows * 128);
+  const int e = lane & 31, hf = lane >> 5;
+  float qv[CGRAM32_ROWS / 2], cv[CGRAM32_ROWS / 2];
+#pragma unroll
+  for (int s = 0; s < CGRAM32_ROWS / 2; s++) {
+    const int r = 2 * s + hf;  // rows past n: weight 0, the load reads zero
+    const uint32_t i = (uint32_t)__shfl((int)il, r, 64);
+    cv[s] = __shfl(cl, r, 64);
+    qv[s] = bld1<float>(qb, r < n ? i * 128u + (uint32_t)e * 4u : 0xffffffffu);
+  }
+  f16x acc;
+#pragma unroll
+  for (int r = 0; r < 16; r++) acc[r] = 0.0f;
+#pragma unroll
+  for (int s = 0; s < CGRAM32_ROWS / 2; s++)
+    if (2 * s < n) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cv[s] * qv[s], qv[s], acc, 0, 0, 0);
+  // D register r of lane l: element m = 8(r/4) + 4(l/32) + r%4, n = l%32
+  float *out = jb.nparts <= 1 ? G + (size_t)jb.col * 1024 : gpart + (size_t)jb.slot * 1024;
+#pragma unroll
+  for (int r = 0; r < 16; r++) out[(8 * (r >> 2) + 4 * hf + (r & 3)) * 32 + e] = acc[r];
+}
+
+// G_c = sum of the partial slots of a multi-chunk column, in slot order
+// (sums: Job{col, nparts, first slot}).  One block per such column; thread t
+// owns elements 4t .. 4t+3; slots are read GB at a time (loads in flight).
+static __global__ __launch_bounds__(BLOCK) void k_gram_slot_sum(const Job *__restrict__ sums,
+                                                         const float *__restrict__ gpart, float *__restrict__ G) {
+  constexpr int GB = 8;
+  const Job jb = sums[blockIdx.x];
+  const f4v *src = reinterpret_cast<const f4v *>(gpart + (size_t)jb.slot * 1024) + threadIdx.x;
+  f4v acc = src[0];
+  for (uint32_t q0 = 1; q0 < jb.nparts; q0 += GB) {
+    f4v y[GB];
+#pragma unroll
+    for (int u = 0; u < GB; u++) y[u] = q0 + u < jb.nparts ? src[(size_t)(q0 + u) * 256] : f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < GB; u++)
+      if (q0 + u < jb.nparts) acc += y[u];
+  }
+  reinterpret_cast<f4v *>(G + (size_t)jb.col * 1024)[threadIdx.x] = acc;
+}
+
 // One CG step of a Gram side half: per column, the direction p_c of
 // iteration f.it (formed from r, Hp, p as col_finalize does), s = G_c p_c,
 // then the Hessian-vector finalisation (MODE 1), or s stored into f.acc for

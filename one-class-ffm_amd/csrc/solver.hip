@@ -105,6 +105,7 @@ template <typename real> struct DevField {
   // Allocated on the first Gram half (col_grams); gpart holds the ordered
   // partial slots of multi-chunk columns (gslots of them).
   DevBuf<Job> gchunks;
+  DevBuf<Job> gsums;  // MFMA build (k_col_gram32): multi-chunk columns {col, nparts, first slot}
   DevBuf<real> gram, gpart;
   uint64_t gslots = 0;
   // Owned field (several ranks): every feature is touched by the
@@ -1536,11 +1537,12 @@ template <typename real> class Problem final : public ProblemBase {
   // column get consecutive partial slots (Job.slot) and their index in the
   // column (Job.flags).  The Gram buffers are allocated by col_grams.
   void col_gram_chunks(DevField<real> &F, const std::vector<uint32_t> &xidx) {
-    const uint64_t ch = std::min<uint64_t>(cgram_chunk_, (uint64_t)cgram_rows((int)kp_, (int)sizeof(real)));
+    const uint64_t ch = cgram32() ? (uint64_t)CGRAM32_ROWS
+                                  : std::min<uint64_t>(cgram_chunk_, (uint64_t)cgram_rows((int)kp_, (int)sizeof(real)));
     std::vector<uint64_t> cptr(F.D + 1, 0);
     for (uint32_t c : xidx) cptr[c + 1]++;
     for (uint64_t d = 0; d < F.D; d++) cptr[d + 1] += cptr[d];
-    std::vector<Job> chunks;
+    std::vector<Job> chunks, sums;
     uint64_t slots = 0;
     for (uint64_t d = 0; d < F.D; d++) {
       const uint64_t b = cptr[d], e = cptr[d + 1];
@@ -1548,12 +1550,17 @@ template <typename real> class Problem final : public ProblemBase {
       for (uint32_t q = 0; q < np; q++)
         chunks.push_back(Job{(uint32_t)d, np, np > 1 ? (uint32_t)(slots + q) : 0u, q,
                              (int64_t)std::min(e, b + q * ch), (int64_t)std::min(e, b + (q + 1) * ch)});
+      if (np > 1) sums.push_back(Job{(uint32_t)d, np, (uint32_t)slots, 0u, 0, 0});
       if (np > 1) slots += np;
     }
     if (slots > 0xffffffffull) throw Error(OCFFM_E_DATA, "too many Gram chunks in one field");
     F.gchunks.upload(chunks);
+    if (cgram32() && !sums.empty()) F.gsums.upload(sums);
     F.gslots = slots;
   }
+
+  // fp32 at KP = 32: the Grams are built on MFMA (kernels.hpp k_col_gram32)
+  bool cgram32() const { return std::is_same<real, float>::value && kp_ == 32 && !no_mfma_; }
 
   // Side half whose CG steps run on per-column Grams (several ranks: each
   // builds its partial Grams, and every CG step all-reduces G_c p_c).
@@ -1585,6 +1592,18 @@ template <typename real> class Problem final : public ProblemBase {
       constexpr int KP = decltype(K)::value;
       const double rs = sizeof(real);
       prof_launch("col_gram", (double)F.nnz * (8 + rs + 16 + KP * rs) + (double)F.gram.bytes(), [&] {
+        if constexpr (std::is_same<real, float>::value && KP == 32) {
+          if (cgram32()) {
+            // (q1: the same-side partner table, one row per row of this side)
+            launch(k_col_gram32, (unsigned)((F.gchunks.n + 3) / 4), BLOCK, 0, (uint64_t)F.gchunks.n,
+                   (const Job *)F.gchunks.p, (const uint32_t *)F.crow.p, (const float *)F.cval.p, hess_cnt(h),
+                   (const float *)h.Q1, (uint64_t)h.own->R, w_, hess_n1(h), (float *)F.gram.p, (float *)F.gpart.p);
+            if (F.gsums.n)
+              launch(k_gram_slot_sum, (unsigned)F.gsums.n, BLOCK, 0, (const Job *)F.gsums.p,
+                     (const float *)F.gpart.p, (float *)F.gram.p);
+            return;
+          }
+        }
         launch(k_col_gram<real, KP>, (unsigned)F.gchunks.n, BLOCK, 0, F.gchunks.p, F.crow.p, F.cval.p,
                hess_cnt(h), h.Q1, w_, hess_n1(h), F.gram.p, F.gpart.p, F.cnt.p);
       });

@@ -103,12 +103,16 @@ def test_gradient_and_hv_kernels(self_side):
 KK_RC = dict(seed=3, m=1500, n=4000, mean=20.0, name="kk_rc")  # ~24 % heavy positives on both sides
 
 
-@pytest.mark.parametrize("env", [{}, {"OCFFM_NO_MFMA": "1"}, {"OCFFM_RC": "1"}])
+@pytest.mark.parametrize("env", [{}, {"OCFFM_NO_MFMA": "1"}, {"OCFFM_RC": "1"}, {"OCFFM_CGRAM": "2"},
+                                 {"OCFFM_CGRAM": "2", "OCFFM_NO_MFMA": "1"}])
 def test_gradient_and_hv_fp32_k32(monkeypatch, env):
     """fp32 at k = 32 (the perf build: the cross halves' k x k Grams on MFMA,
     kernels.hpp k_gram_mfma32; the id-field cross halves row-complete with
-    heavy-row Grams, k_hs_cross_rc, opt-in) against the fp64 oracle: every half's
-    gradient and Hessian-vector product within 1e-4 of its largest entry."""
+    heavy-row Grams, k_hs_cross_rc, opt-in; OCFFM_CGRAM=2: every side half of a
+    one-node field on per-column Grams, built on MFMA by k_col_gram32 with
+    multi-chunk columns summed by k_gram_slot_sum, or by k_col_gram under
+    OCFFM_NO_MFMA) against the fp64 oracle: every half's gradient and
+    Hessian-vector product within 1e-4 of its largest entry."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     ds = synth.kkbox(**KK_RC)
@@ -271,7 +275,7 @@ def test_heavy_columns(precision, cgram, monkeypatch):
         assert abs(gpu_objective(o2, g) - f_ref) <= 1e-3 * abs(f_ref)
 
 
-@pytest.mark.parametrize("ds_name", ["heavy", "kkbox_s", "kkbox_s_fuse2"])
+@pytest.mark.parametrize("ds_name", ["heavy", "kkbox_s", "kkbox_s_fuse2", "kkbox_s_cgram2"])
 def test_fp32_runs_bit_identical(ds_name, monkeypatch):
     """The default fp32 path has no order-dependent float sums (feature
     passes, Gram builds and grid reductions combine in a fixed order): two
@@ -283,6 +287,8 @@ def test_fp32_runs_bit_identical(ds_name, monkeypatch):
     else:
         if ds_name.endswith("fuse2"):  # id-like row passes finalise their columns (chunk_finalize)
             monkeypatch.setenv("OCFFM_FUSE", "2")
+        if ds_name.endswith("cgram2"):  # MFMA per-column Grams (k = 32), multi-chunk slot sums
+            monkeypatch.setenv("OCFFM_CGRAM", "2")
         ds = synth.kkbox(m=3000, n=4000, mean=20.0, seed=11, name="kk_det")
     runs = []
     for _ in range(2):

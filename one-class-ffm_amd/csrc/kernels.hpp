@@ -769,6 +769,57 @@ __global__ __launch_bounds__(BLOCK) void k_init_ytilde(uint64_t R, const int64_t
   }
 }
 
+// T_i = sum_c P_c[i] M_c for every row of a side (the w T_i term of
+// gd_cross, ffm.cpp:663-700), fp32 at KP = 32, on MFMA, before the cross
+// gradient pass (which then loads one T row per row instead of C table rows
+// and C k x k products).  In the pass, T_i cost C k^2 LDS reads per row
+// (4 KB per table: LDS-bound, ~24 KB per row at C = 6) and its registers held
+// the gathers' occupancy down: at kkbox shape the pass ran ~0.5 ms per epoch
+// faster without it.  Here one wave computes a 32-row tile as a 32 x 32 x
+// (C * 32) product: v_mfma_f32_32x32x2f32 with the rows as M and the table
+// columns as K, taken in the order (s, s + 16) so that lane l's A operands
+// are 16 consecutive floats of its row (row l % 32, floats 16 (l / 32) ..
+// + 15: four 16-B loads per table, all issued before the first MFMA); B =
+// M_c (staged once per block in LDS), lane l reads M_c[s + 16 (l / 32)][l % 32].
+template <int L>
+__global__ __launch_bounds__(BLOCK) void k_rows_T32(uint64_t R, const float *const *__restrict__ P,
+                                                    const float *__restrict__ M, float *__restrict__ T) {
+  typedef float f16x __attribute__((ext_vector_type(16)));
+  __shared__ float Ms[L * 1024];
+  for (int t = threadIdx.x; t < L * 1024; t += BLOCK) Ms[t] = M[t];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, e = lane & 31, hf = lane >> 5;
+  BufView pb[L];
+#pragma unroll
+  for (int c = 0; c < L; c++) pb[c] = buf_view(P[c], R * 128);
+  const uint64_t ntiles = (R + 31) / 32;
+  const uint64_t wave = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+  const uint64_t nw = ((uint64_t)gridDim.x * BLOCK) >> 6;
+  for (uint64_t tile = wave; tile < ntiles; tile += nw) {
+    const uint64_t row = tile * 32 + e;  // rows past R read zero (buffer range)
+    f4v a[L][4];
+#pragma unroll
+    for (int c = 0; c < L; c++)
+#pragma unroll
+      for (int q = 0; q < 4; q++) a[c][q] = bld<float>(pb[c], (uint32_t)(row * 128 + hf * 64 + q * 16));
+    f16x acc;
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[r] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < L; c++)
+#pragma unroll
+      for (int s = 0; s < 16; s++)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c][s >> 2][s & 3], Ms[c * 1024 + (s + 16 * hf) * 32 + e], acc, 0,
+                                                   0, 0);
+    // D register r of lane l: row m = 8(r/4) + 4(l/32) + r%4 of the tile, column l%32
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const uint64_t m = tile * 32 + 8 * (r >> 2) + 4 * hf + (r & 3);
+      if (m < R) T[m * 32 + e] = acc[r];
+    }
+  }
+}
+
 // --------------------------------------------------------- gradient rows ---
 // Positive-gather row kernels run ONE SEGMENT PER SUBGROUP (LPR lanes): a
 // wave keeps NSG segments in flight, each walking its (<= 32) positives with
@@ -785,7 +836,7 @@ __global__ __launch_bounds__(BLOCK) void k_init_ytilde(uint64_t R, const int64_t
 // row's feature column itself (col_arrive / col_finalize, MODE 0).
 enum { BM_FULL = 0, BM_IN = 1, BM_ENTER = 2 };  // base modes of k_gd_cross_seg
 
-template <typename real, int KP, bool MLDS, bool FUSE, int BM>
+template <typename real, int KP, bool MLDS, bool FUSE, int BM, bool TP = false>
 __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                         const uint32_t *__restrict__ ycol,
                                                         real *__restrict__ yt, const real *__restrict__ Q1,
@@ -800,9 +851,11 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
                                                         const real *__restrict__ cur,
                                                         const real *__restrict__ drow,
                                                         const real *__restrict__ dxs, real *__restrict__ yt_other,
-                                                        const uint32_t *__restrict__ perm) {
+                                                        const uint32_t *__restrict__ perm,
+                                                        const real *__restrict__ Tpre) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP, OCFFM_GD_GB>;
+  // TP: T_i precomputed by k_rows_T32 (one row load; no M in LDS)
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real)), bb = buf_view(b1, q1rows * sizeof(real));
   const BufView xb = buf_view(dxs, dxs ? q1rows * KP * sizeof(real) : 0);
   extern __shared__ __align__(16) unsigned char smem_raw[];
@@ -810,7 +863,7 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
   const real *Mp = M;
   // TL: T_i by lane-local accumulation over transposed M (fp32, KP <= 32)
   constexpr bool TL = MLDS && std::is_same<real, float>::value && KP <= 32;
-  if (MLDS) {
+  if (MLDS && !TP) {
     const int tot = C * KP * KP;
     for (int t = threadIdx.x; t < tot; t += BLOCK) {
       if constexpr (TL) {  // pair-transposed (lane_vecmat_acc)
@@ -904,7 +957,15 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
         }
       }
     }
-    if (seg_first(sgm)) {
+    if (TP && seg_first(sgm)) {
+      const real z = ai - (real)r;
+      pk += vsplat<real>((real)w) * (vld<real>(Tpre + i * KP + li * G::VE) + vsplat<real>(z) * oQ + bQ);
+    }
+#ifdef OCFFM_EXP_NO_TI
+    if (false) {  // timing experiment only: T_i skipped (wrong results)
+#else
+    if (!TP && seg_first(sgm)) {
+#endif
       // T_i: the C row loads are independent; issue them in batches so the
       // vector-matrix products do not wait on one HBM round trip per table
       constexpr int CB = 4;
@@ -967,8 +1028,47 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
   }
 }
 
+// Per segment s: ysum[s] = sum_{p in seg} (base_p + b1[ycol_p]).  A side's
+// gradient passes (gd_side) need sum_{j in seg} y~_ij = ysum[s] + n_s a_i
+// (y~ = base + a_i + b_j), and over the side halves of one side
+// neither the base nor the partner biases b change (side updates only move
+// this side's a): the solver computes ysum once per side phase and the
+// gradient passes then touch no positive (k_gd_side_seg PRE).
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_seg_ysum(uint64_t nseg, const Seg *__restrict__ segs,
+                                                    const uint32_t *__restrict__ ycol, const real *__restrict__ yt,
+                                                    const real *__restrict__ b1, uint64_t nb1,
+                                                    real *__restrict__ ysum) {
+  using G = Geo<real, KP>;
+  using PP = PosPass<real, KP>;
+  const BufView bb = buf_view(b1, nb1 * sizeof(real));
+  WAVE_SETUP
+  const int sg = lane / G::LPR, li = lane % G::LPR;
+  for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) {
+    const Seg sgm = segs[s];
+    real z = 0;
+    for (int64_t p0 = sgm.b; p0 < sgm.e; p0 += PP::PW) {
+      uint32_t jj[PP::UT];
+      real yv[PP::UT], cb[PP::UT];
+      PP::load_cols(ycol, p0, sgm.e, li, jj);
+#pragma unroll
+      for (int t = 0; t < PP::UT; t++) {
+        const int64_t q = p0 + li + t * G::LPR;
+        yv[t] = q < sgm.e ? yt[q] : (real)0;
+        cb[t] = bld1<real>(bb, jj[t] == POS_NONE ? bb.oob : jj[t] * (uint32_t)sizeof(real));
+      }
+#pragma unroll
+      for (int t = 0; t < PP::UT; t++)
+        if (p0 + li + t * G::LPR < sgm.e) z += yv[t] + cb[t];
+    }
+    z = sg_sum<G::LPR>(z);
+    if (li == 0) ysum[s] = z;
+  }
+}
+
 // Per segment: h[s] = zpart * q1_i, zpart = sum_{p in seg} ((1-w) y~ - w (1-r))
 // + [first] w (n1 (a_i - r) + sum(b) + sa_i)   (gd_side row body, ffm.cpp:572-589).
+// ysum non-null: the positive sum comes from k_seg_ysum (no positive pass).
 template <typename real, int KP, bool FUSE>
 __global__ __launch_bounds__(BLOCK) void k_gd_side_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                        const uint32_t *__restrict__ ycol,
@@ -980,7 +1080,8 @@ __global__ __launch_bounds__(BLOCK) void k_gd_side_seg(uint64_t nseg, const Seg 
                                                        const int64_t *__restrict__ xptr,
                                                        const uint32_t *__restrict__ xidx,
                                                        const real *__restrict__ xval, uint64_t nb1, Fin<real> f,
-                                                       const uint32_t *__restrict__ segptr) {
+                                                       const uint32_t *__restrict__ segptr,
+                                                       const real *__restrict__ ysum) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP>;
   const BufView bb = buf_view(b1, nb1 * sizeof(real));
@@ -989,10 +1090,14 @@ __global__ __launch_bounds__(BLOCK) void k_gd_side_seg(uint64_t nseg, const Seg 
   const real cpos = (real)(1 - w), cneg = (real)(w * (1 - r));
   const double bs = *bsum;
   double dsum[3] = {0, 0, 0};
-  auto body = [&](const Seg &sgm) -> vec_t<real> {
+  auto body = [&](const Seg &sgm, uint64_t s) -> vec_t<real> {
     const uint64_t i = sgm.row;
     const real ai = a1[i];
     real z = 0;
+    if (ysum) {  // sum_{p in seg} ((1-w)(base + a_i + b_j) - w(1-r)), summed once per side phase
+      const real n = (real)(sgm.e - sgm.b);
+      z = cpos * (ysum[s] + n * ai) - n * cneg;
+    } else {
     for (int64_t p0 = sgm.b; p0 < sgm.e; p0 += PP::PW) {
       uint32_t jj[PP::UT];
       real yv[PP::UT], cb[PP::UT];
@@ -1008,11 +1113,12 @@ __global__ __launch_bounds__(BLOCK) void k_gd_side_seg(uint64_t nseg, const Seg 
         if (p0 + li + t * G::LPR < sgm.e) z += cpos * (yv[t] + ai + cb[t]) - cneg;
     }
     z = sg_sum<G::LPR>(z);
+    }
     if (seg_first(sgm)) z += (real)(w * (n1 * ((double)ai - r) + bs + (double)sa1[i]));
     return vsplat<real>(z) * vld<real>(Q1 + i * KP + li * G::VE);
   };
   if constexpr (!FUSE) {
-    for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) vst<real>(h + s * KP + li * G::VE, body(segs[s]));
+    for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) vst<real>(h + s * KP + li * G::VE, body(segs[s], s));
   } else {  // id-like field: the row pass finalises its columns (chunk_finalize)
     __shared__ __align__(16) real hw[BLOCK / 64][G::NSG * KP];
     __shared__ uint32_t hr[BLOCK / 64][G::NSG];
@@ -1029,7 +1135,7 @@ __global__ __launch_bounds__(BLOCK) void k_gd_side_seg(uint64_t nseg, const Seg 
         row = sgm.row;
         nrow = seg_nrow(sgm);
         col = xidx[row];
-        out = vsplat<real>(xval[row]) * body(sgm);
+        out = vsplat<real>(xval[row]) * body(sgm, s);
       }
       chunk_finalize<real, KP, 0>(f, c, sg, li, valid, row, out, col, segptr, nrow, h, nchunk, (real)0, (real)0, false,
                                   dsum, hw[wv], hr[wv], lq[wv]);

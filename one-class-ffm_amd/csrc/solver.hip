@@ -414,6 +414,8 @@ template <typename real> class Problem final : public ProblemBase {
     if (comm_.host_fn) HIPCHK(hipHostMalloc((void **)&dstage_, DSTAGE * sizeof(double), hipHostMallocDefault));
     dots_.alloc(4);
     bsum_.alloc(2);
+    ysum_.alloc(std::max<uint64_t>(std::max(U_.nseg, V_.nseg), 1));
+    if (tpre(Rmax)) Tpre_.alloc(Rmax * kp_);
   }
 
   ~Problem() override {
@@ -446,6 +448,7 @@ template <typename real> class Problem final : public ProblemBase {
   std::chrono::steady_clock::time_point tmark_t_;
 
   void init() override {
+    ysum_dirty();
     tmark(nullptr);
     const size_t rs = sizeof(real);
     std::vector<double> host;
@@ -742,6 +745,7 @@ template <typename real> class Problem final : public ProblemBase {
   }
 
   void set(char what, uint32_t b12, const double *in, uint64_t len) override {
+    ysum_dirty();
     need_init();
     if (b12 >= blocks_.size() || !blocks_[b12].used) throw Error(OCFFM_E_ARG, "block not in the model");
     const Block &b = blocks_[b12];
@@ -1376,6 +1380,7 @@ template <typename real> class Problem final : public ProblemBase {
     DevSide<real> &own = *h.own;
     const bool fz_ = fused_rows(h, false);
     if (!(lazy_ok_ && h.cross)) flush_base();  // this half reads (or updates) the full base
+    if (h.cross) ysum_dirty();                   // (entering a block rewrites the stored base)
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
       using Gm = Geo<real, KP>;
@@ -1405,15 +1410,48 @@ template <typename real> class Problem final : public ProblemBase {
         // cur / drow are rows of the C tables already counted; entering stores e
         // and gathers the previous block's partner rows
         if (enter) bytes += (double)own.npos * rs + (dxs ? (double)ps.R * KP * rs : 0);
+        // T_i = sum_c P_c[i] M_c on MFMA ahead of the pass (k_rows_T32)
+        const bool tp = tpre(own.R);
+        if (tp) {
+          if constexpr (std::is_same<real, float>::value && KP == 32) {
+            prof_launch("rows_T", (double)C_ * own.R * KP * rs + (double)own.R * KP * rs + (double)C_ * KP * KP * rs, [&] {
+              auto gt = [&](auto lc) {
+                constexpr int LC = decltype(lc)::value;
+                launch(k_rows_T32<LC>, grid_for((own.R + 31) / 32, 4, tpre_blocks_), BLOCK, 0, (uint64_t)own.R,
+                       (const float *const *)(tabs_.p + (h.user ? 0 : C_)), (const float *)M_.p, (float *)Tpre_.p);
+              };
+              switch (C_) {  // the table count is a compile-time constant of the kernel
+                case 1: gt(std::integral_constant<int, 1>()); break;
+                case 2: gt(std::integral_constant<int, 2>()); break;
+                case 3: gt(std::integral_constant<int, 3>()); break;
+                case 4: gt(std::integral_constant<int, 4>()); break;
+                case 5: gt(std::integral_constant<int, 5>()); break;
+                case 6: gt(std::integral_constant<int, 6>()); break;
+                case 7: gt(std::integral_constant<int, 7>()); break;
+                default: gt(std::integral_constant<int, 8>()); break;
+              }
+            });
+          }
+        }
         auto go2 = [&](auto fz, auto ml, auto bm) {
           constexpr bool FZ = decltype(fz)::value, ML = decltype(ml)::value;
           constexpr int BM = decltype(bm)::value;
-          launch(k_gd_cross_seg<real, KP, ML, FZ, BM>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : gd_blocks_), BLOCK, ML ? msz : 0,
-              own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
-              (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, h.partner->bias.p, w_,
-              r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, (uint64_t)h.partner->R, fin, (const uint32_t *)own.segptr.p,
-              cur, drow, dxs, (enter && lazy_scatter_) ? h.partner->yt.p : (real *)nullptr,
-              (const uint32_t *)own.perm.p);
+          auto go3 = [&](auto tpc) {
+            constexpr bool TP = decltype(tpc)::value;
+            launch(k_gd_cross_seg<real, KP, ML, FZ, BM, TP>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : gd_blocks_), BLOCK,
+                TP ? 0 : (ML ? msz : 0), own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
+                (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, h.partner->bias.p, w_,
+                r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, (uint64_t)h.partner->R, fin, (const uint32_t *)own.segptr.p,
+                cur, drow, dxs, (enter && lazy_scatter_) ? h.partner->yt.p : (real *)nullptr,
+                (const uint32_t *)own.perm.p, TP ? (const real *)Tpre_.p : (const real *)nullptr);
+          };
+          if constexpr (std::is_same<real, float>::value && KP == 32 && ML) {
+            if (tp) {
+              go3(std::true_type());
+              return;
+            }
+          }
+          go3(std::false_type());
         };
         auto go = [&](auto fz, auto ml) {
           if (!cur) go2(fz, ml, std::integral_constant<int, BM_FULL>());
@@ -1436,15 +1474,26 @@ template <typename real> class Problem final : public ProblemBase {
       } else {
         DevSide<real> &other = h.user ? V_ : U_;  // bsum_: sum of the other side's bias (b_sum, ffm.cpp:551)
         const double n1 = (double)other.R;
-        const double bytes = (double)own.R * 8 + (double)own.npos * rs + (double)own.R * KP * rs * 2 +
-                             (double)own.R * rs * 2;
+        // (with the segment sums: one sum per segment instead of the positives)
+        const double bytes = (double)own.R * 8 + (ysum_on_ ? (double)own.nseg * (16 + rs) : (double)own.npos * rs) +
+                             (double)own.R * KP * rs * 2 + (double)own.R * rs * 2;
         DevField<real> &F = *h.F;
         const Fin<real> fin = make_fin(h, 0);
+        // segment sums of base + partner bias: once per side phase (k_seg_ysum)
+        const int ys = h.user ? 0 : 1;
+        if (ysum_on_ && !ysum_ok_[ys] && own.nseg) {
+          prof_launch("seg_ysum", (double)own.npos * (4 + 2 * rs) + (double)own.nseg * (16 + rs), [&] {
+            launch(k_seg_ysum<real, KP>, grid_for(own.nseg, 4 * Gm::NSG), BLOCK, 0, own.nseg, own.segs.p,
+                   own.ycol.p, (const real *)own.yt.p, (const real *)other.bias.p, (uint64_t)other.R, ysum_.p);
+          });
+          ysum_ok_[ys] = true;
+        }
+        const real *ysum = ysum_on_ ? (const real *)ysum_.p : nullptr;
         auto go = [&](auto fz) {
           constexpr bool FZ = decltype(fz)::value;
           launch(k_gd_side_seg<real, KP, FZ>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, 0,
               own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, own.bias.p, other.bias.p, own.s.p, bsum_.p + (h.user ? 1 : 0),
-              n1, w_, r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, (uint64_t)other.R, fin, (const uint32_t *)own.segptr.p);
+              n1, w_, r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, (uint64_t)other.R, fin, (const uint32_t *)own.segptr.p, ysum);
         };
         prof_launch(fz_ ? "gd_side_fused" : "gd_side_row", bytes, [&] {
           if (fz_) go(std::true_type());
@@ -1463,6 +1512,7 @@ template <typename real> class Problem final : public ProblemBase {
   // (k_update_cross_seg with XS = P_b), then the refresh of the other one.
   void flush_base() {
     if (!excl_.on) return;
+    ysum_dirty();
     excl_.on = false;
     const Block &b = blocks_[excl_.b12];
     DevSide<real> &own = U_, &other = V_;
@@ -1487,6 +1537,7 @@ template <typename real> class Problem final : public ProblemBase {
 
   // other.yt (base in the other orientation) := own.yt through other.perm.
   void refresh_other(DevSide<real> &own, DevSide<real> &other, const int *skip = nullptr) {
+    ysum_dirty();
     if (!other.npos) return;
     prof_launch("refresh_base", (double)other.npos * (4 + 2 * sizeof(real)), [&] {
       launch(k_gather_pos<real>, grid_for((other.npos + 3) / 4, BLOCK, 4096), BLOCK, 0, (uint64_t)other.npos,
@@ -1931,6 +1982,10 @@ template <typename real> class Problem final : public ProblemBase {
   // a speculative update, whose kernels return at entry when *skip is set.
   void finish_half(HalfCtx &h, const int *skip) {
     DevSide<real> &own = *h.own;
+    // a cross update moves the base; a side update moves this side's bias,
+    // which the other side's segment sums hold (k_seg_ysum)
+    if (h.cross) ysum_dirty();
+    else ysum_ok_[h.user ? 1 : 0] = false;
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
       using Gm = Geo<real, KP>;
@@ -2026,6 +2081,25 @@ template <typename real> class Problem final : public ProblemBase {
   // speculative update at the previous epoch's CG count (OCFFM_SPEC=0: off)
   bool spec_on_ = !std::getenv("OCFFM_SPEC") || std::atoi(std::getenv("OCFFM_SPEC")) != 0;
   std::vector<int> pred_;  // per (block, half): CG count of the last solve
+  // Segment sums of base + partner bias for the side gradient passes
+  // (k_seg_ysum); [0] user rows, [1] item rows.  OCFFM_YSUM=0: the passes
+  // walk their positives every time.
+  bool ysum_on_ = !std::getenv("OCFFM_YSUM") || std::atoi(std::getenv("OCFFM_YSUM")) != 0;
+  bool ysum_ok_[2] = {false, false};
+  // T_i of the cross gradient passes precomputed on MFMA (k_rows_T32; fp32,
+  // KP = 32, at most 8 cross tables).  Opt-in (OCFFM_TPRE=1): measured a wash
+  // at kkbox shape (the pass gets 25 / 13 us faster per item / user
+  // half, the pre-pass costs 26.8 / 10.8 us: it must read the C tables' rows,
+  // 77 MB on the item half, which the pass had overlapped with its gathers).
+  bool tpre_on_ = std::getenv("OCFFM_TPRE") && std::atoi(std::getenv("OCFFM_TPRE")) != 0;
+  DevBuf<real> Tpre_;
+  unsigned tpre_blocks_ = std::getenv("OCFFM_TPRE_BLOCKS") ? (unsigned)std::max(1, std::atoi(std::getenv("OCFFM_TPRE_BLOCKS"))) : 512;
+  bool tpre(uint64_t R) const {
+    return tpre_on_ && std::is_same<real, float>::value && kp_ == 32 && C_ >= 1 && C_ <= 8 && R > 0 &&
+           (uint64_t)R * 128 < 0xffffff00ull && (size_t)C_ * kp_ * kp_ * sizeof(real) <= 64 * 1024;
+  }
+  DevBuf<real> ysum_;
+  void ysum_dirty() { ysum_ok_[0] = ysum_ok_[1] = false; }
   // OCFFM_SPEC_FIXED=n (tests): predict n for every half (hits and misses of every kind)
   int spec_fixed_ = std::getenv("OCFFM_SPEC_FIXED") ? std::atoi(std::getenv("OCFFM_SPEC_FIXED")) : 0;
   int fuse_ = 1;

@@ -104,7 +104,7 @@ KK_RC = dict(seed=3, m=1500, n=4000, mean=20.0, name="kk_rc")  # ~24 % heavy pos
 
 
 @pytest.mark.parametrize("env", [{}, {"OCFFM_NO_MFMA": "1"}, {"OCFFM_RC": "1"}, {"OCFFM_CGRAM": "2"},
-                                 {"OCFFM_CGRAM": "2", "OCFFM_NO_MFMA": "1"}])
+                                 {"OCFFM_CGRAM": "2", "OCFFM_NO_MFMA": "1"}, {"OCFFM_TPRE": "1"}])
 def test_gradient_and_hv_fp32_k32(monkeypatch, env):
     """fp32 at k = 32 (the perf build: the cross halves' k x k Grams on MFMA,
     kernels.hpp k_gram_mfma32; the id-field cross halves row-complete with
@@ -338,7 +338,8 @@ def test_speculative_update_bit_identical(monkeypatch):
 @pytest.mark.parametrize("env", [{"OCFFM_FUSE": "2"}, {"OCFFM_FUSE": "0"}, {"OCFFM_SEG_LEN": "3"}, {"OCFFM_LOOKAHEAD": "3"}, {"OCFFM_SCATTER": "1"},
                                  {"OCFFM_FUSE": "2", "OCFFM_SEG_LEN": "2"}, {"OCFFM_CGRAM": "0"},
                                  {"OCFFM_NO_FOLD": "1"}, {"OCFFM_LAZY_BASE": "0"},
-                                 {"OCFFM_SPEC_FIXED": "1"}, {"OCFFM_SPEC_FIXED": "2"}, {"OCFFM_SPEC": "0"}])
+                                 {"OCFFM_SPEC_FIXED": "1"}, {"OCFFM_SPEC_FIXED": "2"}, {"OCFFM_SPEC": "0"},
+                                 {"OCFFM_YSUM": "0"}])
 def test_execution_variants_fp64(kk_small, monkeypatch, env):
     """Schedule knobs (id-field row fusion, segment length, CG look-ahead)
     change the kernels that run, never the result."""

@@ -852,10 +852,14 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
                                                         const real *__restrict__ drow,
                                                         const real *__restrict__ dxs, real *__restrict__ yt_other,
                                                         const uint32_t *__restrict__ perm,
-                                                        const real *__restrict__ Tpre) {
+                                                        const real *__restrict__ Tpre,
+                                                        const real *__restrict__ ytv) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP, OCFFM_GD_GB>;
   // TP: T_i precomputed by k_rows_T32 (one row load; no M in LDS)
+  // ytv (BM_IN): the stored value is read from the other orientation through
+  // perm (ytv[perm[q]]), so the entering pass of the block needs no refresh
+  // of this orientation (solver.hip gradient)
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real)), bb = buf_view(b1, q1rows * sizeof(real));
   const BufView xb = buf_view(dxs, dxs ? q1rows * KP * sizeof(real) : 0);
   extern __shared__ __align__(16) unsigned char smem_raw[];
@@ -911,7 +915,7 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
 #pragma unroll
       for (int t = 0; t < PP::UT; t++) {
         const int64_t q = p0 + li + t * G::LPR;
-        yv[t] = q < sgm.e ? yt[q] : (real)0;
+        yv[t] = q < sgm.e ? (ytv ? ytv[perm[q]] : yt[q]) : (real)0;
       }
       real yn[PP::UT];  // WR: e of this lane's positions
 #pragma unroll

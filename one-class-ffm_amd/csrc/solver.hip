@@ -1410,6 +1410,9 @@ template <typename real> class Problem final : public ProblemBase {
         // cur / drow are rows of the C tables already counted; entering stores e
         // and gathers the previous block's partner rows
         if (enter) bytes += (double)own.npos * rs + (dxs ? (double)ps.R * KP * rs : 0);
+        // inside the block (BM_IN): read the stored value through perm from
+        // the orientation the entering pass wrote (no refresh in between)
+        const bool via = ytvia_ && cur && !enter && !lazy_scatter_;
         // T_i = sum_c P_c[i] M_c on MFMA ahead of the pass (k_rows_T32)
         const bool tp = tpre(own.R);
         if (tp) {
@@ -1443,7 +1446,8 @@ template <typename real> class Problem final : public ProblemBase {
                 (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, h.partner->bias.p, w_,
                 r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, (uint64_t)h.partner->R, fin, (const uint32_t *)own.segptr.p,
                 cur, drow, dxs, (enter && lazy_scatter_) ? h.partner->yt.p : (real *)nullptr,
-                (const uint32_t *)own.perm.p, TP ? (const real *)Tpre_.p : (const real *)nullptr);
+                (const uint32_t *)own.perm.p, TP ? (const real *)Tpre_.p : (const real *)nullptr,
+                via ? (const real *)h.partner->yt.p : (const real *)nullptr);
           };
           if constexpr (std::is_same<real, float>::value && KP == 32 && ML) {
             if (tp) {
@@ -1467,7 +1471,9 @@ template <typename real> class Problem final : public ProblemBase {
             else go(std::false_type(), std::false_type());
           }
         });
-        if (enter && !lazy_scatter_) refresh_other(own, *h.partner);  // the other orientation
+        // the other orientation: refreshed here, or read through perm by the
+        // block's second half (ytvia_; flush_base refreshes it after the loop)
+        if (enter && !lazy_scatter_ && !ytvia_) refresh_other(own, *h.partner);
         // QTQ for CG = M of this block (M_ is not rewritten before the half ends)
         const uint32_t c0 = cross_slot(std::min(h.fl, h.fo), std::max(h.fl, h.fo));
         qtq_ = M_.p + (size_t)c0 * KP * KP;
@@ -2086,6 +2092,10 @@ template <typename real> class Problem final : public ProblemBase {
   // walk their positives every time.
   bool ysum_on_ = !std::getenv("OCFFM_YSUM") || std::atoi(std::getenv("OCFFM_YSUM")) != 0;
   bool ysum_ok_[2] = {false, false};
+  // Cross loop: the item halves read the block-excluded value through perm
+  // from the user orientation (k_gd_cross_seg ytv) instead of a refresh after
+  // each entering pass.  OCFFM_YTVIA=0: refresh.
+  bool ytvia_ = !std::getenv("OCFFM_YTVIA") || std::atoi(std::getenv("OCFFM_YTVIA")) != 0;
   // T_i of the cross gradient passes precomputed on MFMA (k_rows_T32; fp32,
   // KP = 32, at most 8 cross tables).  Opt-in (OCFFM_TPRE=1): measured a wash
   // at kkbox shape (the pass gets 25 / 13 us faster per item / user

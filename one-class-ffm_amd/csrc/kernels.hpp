@@ -56,6 +56,9 @@ constexpr int BLOCK = 256;   // 4 waves
 #ifndef OCFFM_GD_GB
 #define OCFFM_GD_GB 8  // partner-row gathers per round in k_gd_cross_seg
 #endif
+#ifndef OCFFM_HS_GB
+#define OCFFM_HS_GB 32  // partner-row gathers per round in k_hs_cross_seg
+#endif
 #ifndef OCFFM_GD_OCC
 #define OCFFM_GD_OCC 1
 #endif
@@ -1430,7 +1433,7 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
                                                         const real *__restrict__ segx, Fin<real> f,
                                                         const uint32_t *__restrict__ segptr) {
   using G = Geo<real, KP>;
-  using PP = PosPass<real, KP, 32>;  // one round of gathers per <= 32-positive segment
+  using PP = PosPass<real, KP, OCFFM_HS_GB>;  // gathers per round (32: one round per <= 32-positive segment)
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real));
   if (run && !*run) return;
   const bool upd = st && it > 1;

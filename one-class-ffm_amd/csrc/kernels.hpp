@@ -2173,7 +2173,7 @@ __global__ __launch_bounds__(BLOCK) void k_gram_part(uint64_t Rp, int L, const r
 template <int L>
 __global__ __launch_bounds__(BLOCK) void k_gram_mfma32(uint64_t Rp, const float *const *__restrict__ A,
                                                       const float *__restrict__ B, const float *__restrict__ wv,
-                                                      double *__restrict__ part, uint64_t rows_per_block) {
+                                                      float *__restrict__ part, uint64_t rows_per_block) {
   typedef float f16x __attribute__((ext_vector_type(16)));
   constexpr int U = 4;  // row pairs per wave per round
   __shared__ float red[L][1024];
@@ -2249,29 +2249,31 @@ __global__ __launch_bounds__(BLOCK) void k_gram_mfma32(uint64_t Rp, const float 
     __syncthreads();
   }
   const size_t NOUT = (size_t)L * 1024 + 2 * 32 + 1;
-  double *out = part + (size_t)blockIdx.x * NOUT;
-  for (int o = threadIdx.x; o < L * 1024; o += BLOCK) out[o] = (double)red[o >> 10][o & 1023];
+  float *out = part + (size_t)blockIdx.x * NOUT;  // f32 partials (k_reduce_parts<real, float>)
+  for (int o = threadIdx.x; o < L * 1024; o += BLOCK) out[o] = red[o >> 10][o & 1023];
   if (threadIdx.x < 32) {
-    out[(size_t)L * 1024 + threadIdx.x] = (double)redc[0][threadIdx.x];
-    out[(size_t)L * 1024 + 32 + threadIdx.x] = (double)redc[1][threadIdx.x];
+    out[(size_t)L * 1024 + threadIdx.x] = redc[0][threadIdx.x];
+    out[(size_t)L * 1024 + 32 + threadIdx.x] = redc[1][threadIdx.x];
   }
-  if (threadIdx.x == 0) out[(size_t)L * 1024 + 64] = (double)redc[2][0];
+  if (threadIdx.x == 0) out[(size_t)L * 1024 + 64] = redc[2][0];
 }
 
 // o in [0, cnt): t = sum_b part[b][off + o]; o < split -> out_real[o] = t,
 // else out_dbl[o - split] = t.  A block owns 16 consecutive outputs
 // (coalesced 128-B reads) and 16 groups of partial rows; groups are combined
 // in fixed order through LDS (deterministic).
-template <typename real>
+// PT: the partials' type (double; float for k_gram_mfma32, whose partials
+// are f32 MFMA accumulators: half the bytes, the same values).
+template <typename real, typename PT = double>
 __global__ __launch_bounds__(BLOCK) void k_reduce_parts(uint64_t nb, uint64_t nout, uint64_t off, uint64_t cnt,
-                                                        const double *__restrict__ part, uint64_t split,
+                                                        const PT *__restrict__ part, uint64_t split,
                                                         real *__restrict__ out_real, double *__restrict__ out_dbl) {
   __shared__ double sh[16][17];
   const int to = threadIdx.x & 15, tg = threadIdx.x >> 4;
   const uint64_t o = (uint64_t)blockIdx.x * 16 + to;
   double s = 0;
   if (o < cnt) {
-    const double *p = part + off + o;
+    const PT *p = part + off + o;
     uint64_t b = tg;
     for (; b + 48 < nb; b += 64) {
       const double x0 = p[b * nout], x1 = p[(b + 16) * nout], x2 = p[(b + 32) * nout], x3 = p[(b + 48) * nout];

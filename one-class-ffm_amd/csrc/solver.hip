@@ -1233,7 +1233,7 @@ template <typename real> class Problem final : public ProblemBase {
         prof_launch("aggregates", abytes, [&] {
           auto go = [&](auto lc) {
             launch(k_gram_mfma32<decltype(lc)::value>, (unsigned)nbx, BLOCK, 0, Rp, (const float *const *)A,
-                   (const float *)B, (const float *)wv, part_.p, rpbm);
+                   (const float *)B, (const float *)wv, (float *)part_.p, rpbm);
           };
           switch (L) {  // the table count is a compile-time constant of the kernel
             case 1: go(std::integral_constant<int, 1>()); break;
@@ -1256,9 +1256,13 @@ template <typename real> class Problem final : public ProblemBase {
       const uint64_t ng = (uint64_t)L * KP * KP;
       const uint64_t gm = M ? ng : 0, off = M ? 0 : ng, cnt = gm + (sums ? 2 * KP + 1 : 0);
       if (cnt)
-        prof_launch("aggr_reduce", (double)nbx * cnt * 8, [&] {
-          launch(k_reduce_parts<real>, (unsigned)((cnt + 15) / 16), BLOCK, 0, nbx, nout, off, cnt, part_.p, gm, M,
-                 sums_.p);
+        prof_launch("aggr_reduce", (double)nbx * cnt * (mg ? 4 : 8), [&] {
+          if (mg)  // f32 partials (k_gram_mfma32)
+            launch(k_reduce_parts<real, float>, (unsigned)((cnt + 15) / 16), BLOCK, 0, nbx, nout, off, cnt,
+                   (const float *)part_.p, gm, M, sums_.p);
+          else
+            launch(k_reduce_parts<real>, (unsigned)((cnt + 15) / 16), BLOCK, 0, nbx, nout, off, cnt,
+                   (const double *)part_.p, gm, M, sums_.p);
         });
       HIPCHK(hipGetLastError());
     });

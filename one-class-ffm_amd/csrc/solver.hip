@@ -1694,6 +1694,7 @@ template <typename real> class Problem final : public ProblemBase {
            (size_t)kp_ * kp_ * sizeof(real) <= COLTAU_LDS;
   }
 
+  // fuse_ 3: both row passes of side halves (gradient and Hessian-vector).
   // fuse_ 1: the Hessian-vector pass of side halves only (one row = one
   // feature, no partial sums); 2: every row pass of an id-like field (the
   // gradient passes and the cross halves walk positive segments: a row's
@@ -1701,7 +1702,9 @@ template <typename real> class Problem final : public ProblemBase {
   // last-arriver sum when the row spans several chunks, kernels.hpp
   // chunk_finalize).
   bool fused_rows(const HalfCtx &h, bool hv) const {
-    return h.F->idlike && (!comm_.active() || (hv && repl(h))) && (fuse_ >= 2 || (fuse_ == 1 && hv && !h.cross));
+    const bool side = !h.cross;
+    return h.F->idlike && (!comm_.active() || (hv && repl(h))) &&
+           (fuse_ == 2 || (side && (fuse_ == 3 || (fuse_ == 1 && hv))));
   }
 
   // Several ranks, id-like field (replicated rows, e.g. items; never an owned

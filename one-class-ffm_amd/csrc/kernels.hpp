@@ -1415,6 +1415,65 @@ __global__ __launch_bounds__(BLOCK) void k_hv_cgram(uint64_t D, const real *__re
   if constexpr (MODE != 2) fin_blocks<real, 1>(f, dsum);
 }
 
+// The whole Newton-CG solve of a Gram side half with few columns (genre:
+// D = 50) in ONE block of CGS_THREADS threads, one column per subgroup: each
+// iteration is the k_hv_cgram body (direction, G_c p_c, the MODE 1
+// finalisation), a block reduction in wave order and the CG scalars
+// (cg_publish, by thread 0; alpha / beta / the next verdict reach the other
+// waves through LDS).  No grid reduction, launch or host round trip per CG
+// step; the verdicts still reach the host words as they are decided, and the
+// state left behind is the lazy convention's (S without the last alpha p,
+// which k_apply / the update kernels add), as after the per-step launches.
+constexpr int CGS_THREADS = 1024;
+template <typename real, int KP>
+__global__ __launch_bounds__(CGS_THREADS) void k_cg_gram_small(uint64_t D, const real *__restrict__ G, Fin<real> f) {
+  using Gm = Geo<real, KP>;
+  constexpr int NW = CGS_THREADS / 64;
+  __shared__ double sh[3][NW];
+  __shared__ int s_go;
+  __shared__ double s_ab[2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int sg = lane / Gm::LPR, li = lane % Gm::LPR;
+  const uint64_t c = (uint64_t)w * Gm::NSG + sg;  // host: D <= NW * NSG
+  if (threadIdx.x == 0) s_go = f.st->run[1];
+  __syncthreads();
+  int go = s_go;
+  real alpha = 0, beta = 0;
+  for (int it = 1; it <= MAXCG && go; it++) {
+    Fin<real> ft = f;
+    ft.it = it;
+    const bool upd = it > 1;
+    double ds[3] = {0, 0, 0};
+    if (c < D) {
+      const FinOps<real> ops = fin_load<real, KP, 1>(ft, (uint32_t)c, upd, li);
+      vec_t<real> pt = ops.w_or_p;
+      if (upd) pt = (ops.r - vsplat<real>(alpha) * ops.hp) + vsplat<real>(beta) * ops.w_or_p;
+      const vec_t<real> sv = sg_vecmat<real, KP>(pt, G + c * KP * KP, li);
+      col_finalize<real, KP, 1>(ft, (uint32_t)c, sv, alpha, beta, upd, li, ds, ops);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const double v = wave_sum(ds[k]);
+      if (lane == 0) sh[k][w] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double tot[3] = {0, 0, 0};
+      for (int i = 0; i < NW; i++)
+#pragma unroll
+        for (int k = 0; k < 3; k++) tot[k] += sh[k][i];
+      cg_publish<real, 1>(ft, tot);
+      s_go = f.st->run[it + 1];
+      s_ab[0] = f.st->alpha;
+      s_ab[1] = f.st->beta;
+    }
+    __syncthreads();
+    go = s_go;
+    alpha = (real)s_ab[0];
+    beta = (real)s_ab[1];
+  }
+}
+
 // Per segment of row i: h[s] = (1-w) sum_{j in seg} <phi_i, q_j> q_j
 // + [first] w phi_i QTQ, phi_i = X_i p  (hs_cross row body, ffm.cpp:715-738;
 // tau = X_i (V QTQ) = phi_i QTQ).  QTQ staged in LDS; phi_i's components

@@ -1620,6 +1620,16 @@ template <typename real> class Problem final : public ProblemBase {
     F.gslots = slots;
   }
 
+  // A Gram side half with at most one column per subgroup of one
+  // CGS_THREADS block solves its whole CG in one launch (k_cg_gram_small).
+  // Opt-in (OCFFM_CGSMALL=1): measured slower at kkbox shape (DESIGN §7:
+  // 41 us per genre half against ~3 launches of 7.5 us; one CU streams the
+  // Grams and waits out each step's chain alone).
+  bool cgsmall_on_ = std::getenv("OCFFM_CGSMALL") && std::atoi(std::getenv("OCFFM_CGSMALL")) != 0;
+  bool cg_small(const HalfCtx &h) const {
+    return cgsmall_on_ && cgram(h) && !comm_.active() && h.D <= (uint64_t)(CGS_THREADS / 64) * nsg();
+  }
+
   // fp32 at KP = 32: the Grams are built on MFMA (kernels.hpp k_col_gram32)
   bool cgram32() const { return std::is_same<real, float>::value && kp_ == 32 && !no_mfma_; }
 
@@ -1954,7 +1964,24 @@ template <typename real> class Problem final : public ProblemBase {
                                                 : 0;
     bool queued = false;
     const size_t pend0 = pending_.size();
-    for (int it = 1; it <= MAXCG && !done; it++) {
+    if (cg_small(h)) {
+      // the whole solve in one launch (k_cg_gram_small), the update queued
+      // right behind it; the verdicts are read for the log only
+      prof_tag_ = 1;
+      with_kp(kp_, [&](auto K) {
+        constexpr int KP = decltype(K)::value;
+        // (the bytes of one CG step: the launch runs all of them)
+        prof_launch("cg_gram_small", (double)h.D * KP * KP * sizeof(real) + (double)h.D * KP * sizeof(real) * 9, [&] {
+          launch(k_cg_gram_small<real, KP>, 1, CGS_THREADS, 0, (uint64_t)h.D, (const real *)h.F->gram.p,
+                 make_fin(h, 1));
+        });
+      });
+      prof_tag_ = 0;
+      finish_half(h, nullptr);
+      queued = true;
+      examine(MAXCG);
+    }
+    for (int it = 1; it <= MAXCG && !done && !queued; it++) {
       prof_tag_ = it;
       hv_pass(h, it);
       prof_tag_ = 0;

@@ -339,7 +339,8 @@ def test_speculative_update_bit_identical(monkeypatch):
                                  {"OCFFM_FUSE": "2", "OCFFM_SEG_LEN": "2"}, {"OCFFM_CGRAM": "0"},
                                  {"OCFFM_NO_FOLD": "1"}, {"OCFFM_LAZY_BASE": "0"},
                                  {"OCFFM_SPEC_FIXED": "1"}, {"OCFFM_SPEC_FIXED": "2"}, {"OCFFM_SPEC": "0"},
-                                 {"OCFFM_YSUM": "0"}, {"OCFFM_YTVIA": "0"}, {"OCFFM_FUSE": "3"}])
+                                 {"OCFFM_YSUM": "0"}, {"OCFFM_YTVIA": "0"}, {"OCFFM_FUSE": "3"},
+                                 {"OCFFM_CGSMALL": "1"}])
 def test_execution_variants_fp64(kk_small, monkeypatch, env):
     """Schedule knobs (id-field row fusion, segment length, CG look-ahead)
     change the kernels that run, never the result."""

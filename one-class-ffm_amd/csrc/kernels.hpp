@@ -968,11 +968,7 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
       const real z = ai - (real)r;
       pk += vsplat<real>((real)w) * (vld<real>(Tpre + i * KP + li * G::VE) + vsplat<real>(z) * oQ + bQ);
     }
-#ifdef OCFFM_EXP_NO_TI
-    if (false) {  // timing experiment only: T_i skipped (wrong results)
-#else
     if (!TP && seg_first(sgm)) {
-#endif
       // T_i: the C row loads are independent; issue them in batches so the
       // vector-matrix products do not wait on one HBM round trip per table
       constexpr int CB = 4;

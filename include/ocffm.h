@@ -159,6 +159,12 @@ typedef struct ocffm_metrics {
   uint32_t top_k[5];
 } ocffm_metrics;
 int ocffm_problem_validate(ocffm_problem *p, ocffm_metrics *out);
+/* The reference's nDCG known-answer build (-DEBUG_nDCG -DSHOW_SCORE_ONLY,
+ * script/nDCG_degub_tool/readme:1-4): validate() with every test row's
+ * scores forced to z_j = n - j after its ploss term (ffm.cpp:988-993).
+ * per_row_ndcg10 (optional): the nDCG@10 of each of this rank's test rows,
+ * the value that build prints per row (ffm.cpp:1126). */
+int ocffm_problem_validate_forced(ocffm_problem *p, ocffm_metrics *out, double *per_row_ndcg10);
 
 /* print_epoch_info (ffm.cpp:1130-1145) of the last validation, and the
  * header of init_va (ffm.cpp:901-912), to stdout. */
@@ -183,6 +189,16 @@ int ocffm_problem_hv(ocffm_problem *p, uint32_t f1, uint32_t f2, int half, const
 
 /* save_model (ffm.cpp:1163-1237): the reference's text model format. */
 int ocffm_problem_save_model(ocffm_problem *p, const char *path);
+
+/* ImpProblem::save_binary_model (ffm.cpp:1239-1267): W and H of every used
+ * block in the reference's binary layout (uint32 f, fu, fv, k; uint64 Ds;
+ * per block uint32 index_vec, uint64 |W|, uint64 |H|, doubles). */
+int ocffm_problem_save_binary(ocffm_problem *p, const char *path);
+/* ImpProblem::load_binary_model (ffm.cpp:1269-1301) as it was meant to work
+ * (the reference's opens an ofstream and writes): reads that layout, checks
+ * f/fu/fv/k/Ds against this problem, restores W/H and re-derives P, Q, the
+ * biases, sa/sb and y-tilde as ocffm_problem_init does.  May replace init. */
+int ocffm_problem_load_binary(ocffm_problem *p, const char *path);
 
 /* Statistics.  cg: CG iteration count of every half solved since the last
  * reset (solve order).  Kernel timing is recorded with HIP events on the

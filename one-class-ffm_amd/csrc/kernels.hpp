@@ -547,93 +547,6 @@ __device__ __forceinline__ void col_finalize(const Fin<real> &f, uint32_t col, v
   col_finalize<real, KP, MODE>(f, col, s, alpha, beta, upd, li, ds, fin_load<real, KP, MODE>(f, col, upd, li));
 }
 
-// Fused finalisation of an id-like field's row pass over positive segments
-// (the FUSE kernels): deterministic, no float atomics.  A wave walks chunk c
-// of NSG consecutive segments (segments in row order, a row's segments
-// contiguous), one per subgroup, each with its x-scaled output vector `out`.
-// Through the wave's LDS slice (hw: NSG x KP, hr: NSG rows) the first
-// subgroup of each run of same-row segments sums the run in order.  A row
-// whose segments all lie in this chunk is finalised right away (column col);
-// a longer row leaves the run's sum in a slot of chunk c (sc1 stores) and
-// takes a ticket on its column.  A chunk has two slots: 2c+1 for the run of a
-// row that starts in it, 2c for the run of a row that started before it (at
-// most one of each).  When a ticket shows the row's last chunk has arrived,
-// the whole wave sums the row's slots (subgroup t takes chunks c0+t, c0+t+NSG,
-// ... in order, then a fixed cross-subgroup tree; sc1 loads: the guide's
-// last-arriver hand-off) and subgroup 0 finalises: a Pareto-head row of ~1,000
-// segments costs two load rounds, not a serial walk.  Every lane of the wave
-// calls this once per chunk.  lq: 6 words of the wave's LDS.
-template <typename real, int KP, int MODE>
-__device__ __forceinline__ void chunk_finalize(const Fin<real> &f, uint64_t c, int sg, int li, bool valid,
-                                               uint32_t row, vec_t<real> out, uint32_t col,
-                                               const uint32_t *__restrict__ segptr, uint32_t nrow, real *slots,
-                                               uint64_t nchunk, real alpha, real beta, bool upd, double (&ds)[3],
-                                               real *hw, uint32_t *hr, uint32_t *lq) {
-  using G = Geo<real, KP>;
-  constexpr int NSG = G::NSG, VE = G::VE;
-  const int lane = threadIdx.x & 63;
-  *reinterpret_cast<vec_t<real> *>(hw + sg * KP + li * VE) = out;
-  if (li == 0) hr[sg] = valid ? row : 0xffffffffu;
-  if (lane == 0) {
-    lq[0] = 0xffffffffu;  // rows whose last chunk this is: [0] started before c, [1] starts in c
-    lq[3] = 0xffffffffu;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  const bool lead = valid && (sg == 0 || hr[sg - 1] != row);
-  if (lead) {
-    vec_t<real> sum = out;
-    for (int t = sg + 1; t < NSG && hr[t] == row; t++)
-      sum += *reinterpret_cast<const vec_t<real> *>(hw + t * KP + li * VE);
-    const uint64_t s0 = segptr[row];
-    const uint64_t c0 = s0 / NSG, c1 = (s0 + nrow - 1) / NSG;
-    if (c0 == c1) {
-      col_finalize<real, KP, MODE>(f, col, sum, alpha, beta, upd, li, ds);
-    } else {
-      const int kind = c == c0 ? 1 : 0;
-      real *sl = slots + (2 * c + kind) * KP + li * VE;
-#pragma unroll
-      for (int e = 0; e < VE; e++) __hip_atomic_store(sl + e, sum[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (li == 0 && __hip_atomic_fetch_add(f.cnt + col, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                         (unsigned)(c1 - c0)) {
-        lq[3 * kind] = row;
-        lq[3 * kind + 1] = col;
-        lq[3 * kind + 2] = nrow;
-      }
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#pragma unroll
-  for (int kind = 0; kind < 2; kind++) {
-    const uint32_t lrow = lq[3 * kind];
-    if (lrow == 0xffffffffu) continue;  // wave-uniform
-    const uint32_t lcol = lq[3 * kind + 1], lnrow = lq[3 * kind + 2];
-    const uint64_t s0 = segptr[lrow];
-    const uint64_t c0 = s0 / NSG, c1 = (s0 + lnrow - 1) / NSG;
-    const BufView pv = buf_view(slots, 2 * nchunk * KP * sizeof(real));
-    constexpr int RB = 8;
-    vec_t<real> sum = vzero<real>();
-    for (uint64_t q0 = c0 + sg; q0 <= c1; q0 += (uint64_t)RB * NSG) {
-      vec_t<real> y[RB];
-#pragma unroll
-      for (int u = 0; u < RB; u++) {
-        const uint64_t q = q0 + (uint64_t)u * NSG;
-        const uint64_t slot = 2 * q + (q == c0 ? 1 : 0);
-        const uint32_t off = q <= c1 ? (uint32_t)((slot * KP + li * VE) * sizeof(real)) : pv.oob;
-        y[u] = __builtin_bit_cast(vec_t<real>, __builtin_amdgcn_raw_buffer_load_b128(pv.r, off, 0, 16));
-      }
-#pragma unroll
-      for (int u = 0; u < RB; u++) sum += y[u];  // absent slots read zero
-    }
-    sum = xsg_vsum<G::LPR, real>(sum);  // fixed tree over the subgroups
-    if (sg == 0) {
-      col_finalize<real, KP, MODE>(f, lcol, sum, alpha, beta, upd, li, ds);
-      if (li == 0) __hip_atomic_store(f.cnt + lcol, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the LDS slice is rewritten by the next chunk
-}
-
 // Grid-wide end of a finalising kernel.  MODE 0 publishes g2 and the first
 // CG verdict; MODE 1 computes alpha = r2/<p,Hp>, the new r2 (expanded),
 // beta and the verdict for iteration it+1 (ffm.cpp:780, 803-809).
@@ -834,12 +747,9 @@ __global__ __launch_bounds__(BLOCK) void k_rows_T32(uint64_t R, const float *con
 //   h[s] = sum_{j in seg} ((1-w) y~_ij - w (1-r)) q_j
 //          + [first] w (T_i + (a_i - r) oQ + bQ),   T_i = sum_c P_c[i] M_c
 // (gd_cross row body, ffm.cpp:658-700); y~ = base + a_i + b_j.  M in LDS.
-// FUSE (id-like field: one node per row, each feature in exactly one row):
-// the CSC is the identity, so instead of writing h the kernel finalises the
-// row's feature column itself (col_arrive / col_finalize, MODE 0).
 enum { BM_FULL = 0, BM_IN = 1, BM_ENTER = 2 };  // base modes of k_gd_cross_seg
 
-template <typename real, int KP, bool MLDS, bool FUSE, int BM, bool TP = false>
+template <typename real, int KP, bool MLDS, int BM, bool TP = false>
 __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                         const uint32_t *__restrict__ ycol,
                                                         real *__restrict__ yt, const real *__restrict__ Q1,
@@ -847,13 +757,9 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
                                                         const real *__restrict__ M, const double *__restrict__ sums,
                                                         const real *__restrict__ a1, const real *__restrict__ b1,
                                                         double w, double r, real *__restrict__ h,
-                                                        const int64_t *__restrict__ xptr,
-                                                        const uint32_t *__restrict__ xidx,
-                                                        const real *__restrict__ xval, uint64_t q1rows,
-                                                        Fin<real> f, const uint32_t *__restrict__ segptr,
-                                                        const real *__restrict__ cur,
+                                                        uint64_t q1rows, const real *__restrict__ cur,
                                                         const real *__restrict__ drow,
-                                                        const real *__restrict__ dxs, real *__restrict__ yt_other,
+                                                        const real *__restrict__ dxs,
                                                         const uint32_t *__restrict__ perm,
                                                         const real *__restrict__ Tpre,
                                                         const real *__restrict__ ytv) {
@@ -892,7 +798,6 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
     oQ[e] = (real)sums[li * G::VE + e];
     bQ[e] = (real)sums[KP + li * G::VE + e];
   }
-  double dsum[3] = {0, 0, 0};
   // Block-excluded y~.  During the cross loop the stored value is
   // e_ij = y~_ij - <P_b[i], Q_b[j]> for the current cross block b: the halves'
   // updates of P_b / Q_b leave it untouched, and the biases (constant over the
@@ -902,7 +807,7 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
   //   BM_IN   : inside block b; y~ = e + <cur_i, q_j>
   //   BM_ENTER: entering block b; y~ = e' + <drow_i, dxs_j> (e' of block b',
   //             drow/dxs its factors) or base + a_i + b_j (dxs null); stores
-  //             e = y~ - <cur_i, q_j> here (and through perm with yt_other).
+  //             e = y~ - <cur_i, q_j> here.
   constexpr bool WR = BM == BM_ENTER;
   auto body = [&](const Seg &sgm) -> vec_t<real> {
     const uint64_t i = sgm.row;
@@ -957,10 +862,7 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
 #pragma unroll
         for (int t = 0; t < PP::UT; t++) {
           const int64_t q = p0 + li + t * G::LPR;
-          if (q < sgm.e) {
-            yt[q] = yn[t];
-            if (yt_other) yt_other[perm[q]] = yn[t];
-          }
+          if (q < sgm.e) yt[q] = yn[t];
         }
       }
     }
@@ -1004,31 +906,7 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
     }
     return pk;
   };
-  if constexpr (!FUSE) {
-    for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) vst<real>(h + s * KP + li * G::VE, body(segs[s]));
-  } else {  // id-like field: the row pass finalises its columns (chunk_finalize; h holds the chunk slots)
-    __shared__ __align__(16) real hw[BLOCK / 64][G::NSG * KP];
-    __shared__ uint32_t hr[BLOCK / 64][G::NSG];
-    __shared__ uint32_t lq[BLOCK / 64][6];
-    const int wv = threadIdx.x >> 6;
-    const uint64_t nchunk = (nseg + G::NSG - 1) / G::NSG;
-    for (uint64_t c = wave; c < nchunk; c += nwaves) {
-      const uint64_t s = c * G::NSG + sg;
-      const bool valid = s < nseg;
-      vec_t<real> out = vzero<real>();
-      uint32_t row = 0, col = 0, nrow = 1;
-      if (valid) {
-        const Seg sgm = segs[s];
-        row = sgm.row;
-        nrow = seg_nrow(sgm);
-        col = xidx[row];  // id-like: one node per row
-        out = vsplat<real>(xval[row]) * body(sgm);
-      }
-      chunk_finalize<real, KP, 0>(f, c, sg, li, valid, row, out, col, segptr, nrow, h, nchunk, (real)0, (real)0, false,
-                                  dsum, hw[wv], hr[wv], lq[wv]);
-    }
-    fin_blocks<real, 0>(f, dsum);
-  }
+  for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) vst<real>(h + s * KP + li * G::VE, body(segs[s]));
 }
 
 // Per segment s: ysum[s] = sum_{p in seg} (base_p + b1[ycol_p]).  A side's
@@ -1072,18 +950,14 @@ __global__ __launch_bounds__(BLOCK) void k_seg_ysum(uint64_t nseg, const Seg *__
 // Per segment: h[s] = zpart * q1_i, zpart = sum_{p in seg} ((1-w) y~ - w (1-r))
 // + [first] w (n1 (a_i - r) + sum(b) + sa_i)   (gd_side row body, ffm.cpp:572-589).
 // ysum non-null: the positive sum comes from k_seg_ysum (no positive pass).
-template <typename real, int KP, bool FUSE>
+template <typename real, int KP>
 __global__ __launch_bounds__(BLOCK) void k_gd_side_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                        const uint32_t *__restrict__ ycol,
                                                        const real *__restrict__ yt, const real *__restrict__ Q1,
                                                        const real *__restrict__ a1, const real *__restrict__ b1,
                                                        const real *__restrict__ sa1,
                                                        const double *__restrict__ bsum, double n1, double w,
-                                                       double r, real *__restrict__ h,
-                                                       const int64_t *__restrict__ xptr,
-                                                       const uint32_t *__restrict__ xidx,
-                                                       const real *__restrict__ xval, uint64_t nb1, Fin<real> f,
-                                                       const uint32_t *__restrict__ segptr,
+                                                       double r, real *__restrict__ h, uint64_t nb1,
                                                        const real *__restrict__ ysum) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP>;
@@ -1092,7 +966,6 @@ __global__ __launch_bounds__(BLOCK) void k_gd_side_seg(uint64_t nseg, const Seg 
   const int sg = lane / G::LPR, li = lane % G::LPR;
   const real cpos = (real)(1 - w), cneg = (real)(w * (1 - r));
   const double bs = *bsum;
-  double dsum[3] = {0, 0, 0};
   auto body = [&](const Seg &sgm, uint64_t s) -> vec_t<real> {
     const uint64_t i = sgm.row;
     const real ai = a1[i];
@@ -1120,31 +993,7 @@ __global__ __launch_bounds__(BLOCK) void k_gd_side_seg(uint64_t nseg, const Seg 
     if (seg_first(sgm)) z += (real)(w * (n1 * ((double)ai - r) + bs + (double)sa1[i]));
     return vsplat<real>(z) * vld<real>(Q1 + i * KP + li * G::VE);
   };
-  if constexpr (!FUSE) {
-    for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) vst<real>(h + s * KP + li * G::VE, body(segs[s], s));
-  } else {  // id-like field: the row pass finalises its columns (chunk_finalize)
-    __shared__ __align__(16) real hw[BLOCK / 64][G::NSG * KP];
-    __shared__ uint32_t hr[BLOCK / 64][G::NSG];
-    __shared__ uint32_t lq[BLOCK / 64][6];
-    const int wv = threadIdx.x >> 6;
-    const uint64_t nchunk = (nseg + G::NSG - 1) / G::NSG;
-    for (uint64_t c = wave; c < nchunk; c += nwaves) {
-      const uint64_t s = c * G::NSG + sg;
-      const bool valid = s < nseg;
-      vec_t<real> out = vzero<real>();
-      uint32_t row = 0, col = 0, nrow = 1;
-      if (valid) {
-        const Seg sgm = segs[s];
-        row = sgm.row;
-        nrow = seg_nrow(sgm);
-        col = xidx[row];
-        out = vsplat<real>(xval[row]) * body(sgm, s);
-      }
-      chunk_finalize<real, KP, 0>(f, c, sg, li, valid, row, out, col, segptr, nrow, h, nchunk, (real)0, (real)0, false,
-                                  dsum, hw[wv], hr[wv], lq[wv]);
-    }
-    fin_blocks<real, 0>(f, dsum);
-  }
+  for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) vst<real>(h + s * KP + li * G::VE, body(segs[s], s));
 }
 
 // ------------------------------------------------ Hessian-vector rows ---
@@ -1411,70 +1260,11 @@ __global__ __launch_bounds__(BLOCK) void k_hv_cgram(uint64_t D, const real *__re
   if constexpr (MODE != 2) fin_blocks<real, 1>(f, dsum);
 }
 
-// The whole Newton-CG solve of a Gram side half with few columns (genre:
-// D = 50) in ONE block of CGS_THREADS threads, one column per subgroup: each
-// iteration is the k_hv_cgram body (direction, G_c p_c, the MODE 1
-// finalisation), a block reduction in wave order and the CG scalars
-// (cg_publish, by thread 0; alpha / beta / the next verdict reach the other
-// waves through LDS).  No grid reduction, launch or host round trip per CG
-// step; the verdicts still reach the host words as they are decided, and the
-// state left behind is the lazy convention's (S without the last alpha p,
-// which k_apply / the update kernels add), as after the per-step launches.
-constexpr int CGS_THREADS = 1024;
-template <typename real, int KP>
-__global__ __launch_bounds__(CGS_THREADS) void k_cg_gram_small(uint64_t D, const real *__restrict__ G, Fin<real> f) {
-  using Gm = Geo<real, KP>;
-  constexpr int NW = CGS_THREADS / 64;
-  __shared__ double sh[3][NW];
-  __shared__ int s_go;
-  __shared__ double s_ab[2];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int sg = lane / Gm::LPR, li = lane % Gm::LPR;
-  const uint64_t c = (uint64_t)w * Gm::NSG + sg;  // host: D <= NW * NSG
-  if (threadIdx.x == 0) s_go = f.st->run[1];
-  __syncthreads();
-  int go = s_go;
-  real alpha = 0, beta = 0;
-  for (int it = 1; it <= MAXCG && go; it++) {
-    Fin<real> ft = f;
-    ft.it = it;
-    const bool upd = it > 1;
-    double ds[3] = {0, 0, 0};
-    if (c < D) {
-      const FinOps<real> ops = fin_load<real, KP, 1>(ft, (uint32_t)c, upd, li);
-      vec_t<real> pt = ops.w_or_p;
-      if (upd) pt = (ops.r - vsplat<real>(alpha) * ops.hp) + vsplat<real>(beta) * ops.w_or_p;
-      const vec_t<real> sv = sg_vecmat<real, KP>(pt, G + c * KP * KP, li);
-      col_finalize<real, KP, 1>(ft, (uint32_t)c, sv, alpha, beta, upd, li, ds, ops);
-    }
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const double v = wave_sum(ds[k]);
-      if (lane == 0) sh[k][w] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double tot[3] = {0, 0, 0};
-      for (int i = 0; i < NW; i++)
-#pragma unroll
-        for (int k = 0; k < 3; k++) tot[k] += sh[k][i];
-      cg_publish<real, 1>(ft, tot);
-      s_go = f.st->run[it + 1];
-      s_ab[0] = f.st->alpha;
-      s_ab[1] = f.st->beta;
-    }
-    __syncthreads();
-    go = s_go;
-    alpha = (real)s_ab[0];
-    beta = (real)s_ab[1];
-  }
-}
-
 // Per segment of row i: h[s] = (1-w) sum_{j in seg} <phi_i, q_j> q_j
 // + [first] w phi_i QTQ, phi_i = X_i p  (hs_cross row body, ffm.cpp:715-738;
 // tau = X_i (V QTQ) = phi_i QTQ).  QTQ staged in LDS; phi_i's components
 // are broadcast by DPP for the k x k product (sg_vecmat).
-template <typename real, int KP, bool MLDS, bool FUSE>
+template <typename real, int KP, bool MLDS>
 __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                         const int64_t *__restrict__ xptr,
                                                         const uint32_t *__restrict__ xidx,
@@ -1485,8 +1275,7 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
                                                         const int *__restrict__ run, const real *__restrict__ Rv,
                                                         const real *__restrict__ Hv, const CgState *st, int it,
                                                         const uint32_t *__restrict__ segd,
-                                                        const real *__restrict__ segx, Fin<real> f,
-                                                        const uint32_t *__restrict__ segptr) {
+                                                        const real *__restrict__ segx) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP, OCFFM_HS_GB>;  // gathers per round (32: one round per <= 32-positive segment)
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real));
@@ -1505,7 +1294,6 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
   const real cpos = (real)(1 - w);
-  double dsum[3] = {0, 0, 0};
   // Per segment: phi from the row's node(s), the partner-row gathers, tau.
   auto seg_out = [&](const Seg &sgm, uint32_t d1, real x1) -> vec_t<real> {
     const uint64_t i = sgm.row;
@@ -1542,30 +1330,6 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
     }
     return out;
   };
-  if constexpr (FUSE) {  // id-like field: the row pass finalises its columns (chunk_finalize)
-    __shared__ __align__(16) real hw[BLOCK / 64][G::NSG * KP];
-    __shared__ uint32_t hr[BLOCK / 64][G::NSG];
-    __shared__ uint32_t lq[BLOCK / 64][6];
-    const int wv = threadIdx.x >> 6;
-    const uint64_t nchunk = (nseg + G::NSG - 1) / G::NSG;
-    for (uint64_t c = wave; c < nchunk; c += nwaves) {
-      const uint64_t s = c * G::NSG + sg;
-      const bool valid = s < nseg;
-      vec_t<real> out = vzero<real>();
-      uint32_t row = 0, col = 0, nrow = 1;
-      if (valid) {
-        const Seg sgm = segs[s];
-        row = sgm.row;
-        nrow = seg_nrow(sgm);
-        col = segd[s];
-        out = vsplat<real>(segx[s]) * seg_out(sgm, col, segx[s]);
-      }
-      chunk_finalize<real, KP, 1>(f, c, sg, li, valid, row, out, col, segptr, nrow, h, nchunk, alpha, beta, upd, dsum,
-                                  hw[wv], hr[wv], lq[wv]);
-    }
-    fin_blocks<real, 1>(f, dsum);
-    return;
-  }
   // Grid-stride over segments with the next segment's descriptor (and its
   // node) in flight while the current one is gathered.
   const uint64_t stride = nwaves * G::NSG;
@@ -1595,160 +1359,6 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
   }
 }
 
-
-// ------------------------------------------- row-complete cross halves ---
-// Id-like field, one GPU, fp32, KP = 32 ("row-complete"): every
-// row is one work unit, so the Hessian-vector row pass finalises its own
-// feature column and no feature pass runs.  Rows with more than HEAVY_POS
-// positives (the Pareto-head items) use their Gram G_i = sum_{j in pos(i)}
-// q_j q_j^T, built once per half, instead of gathering their partner rows
-// every CG step: (1-w) sum_j <phi, q_j> q_j = (1-w) phi G_i.
-constexpr int HEAVY_POS = 32;
-constexpr int GRAM_CHUNK = 1024;  // positives per Gram partial
-#ifndef RC_GB
-#define RC_GB 8  // partner-row gathers per round in k_hs_cross_rc
-#endif
-struct GChunk {
-  uint32_t heavy;  // index of the heavy row
-  uint32_t pad;
-  int64_t b, e;    // positives
-};
-
-// Partial Gram of one chunk of a heavy row's positives on MFMA
-// (v_mfma_f32_32x32x2f32, A = B = the gathered partner rows: lane l loads
-// Q1[ycol[p + l/32]][l%32], a whole 128-B row per half-wave); the block's
-// four waves take interleaved pairs and are combined in wave order.
-static __global__ __launch_bounds__(BLOCK) void k_pos_gram32(const GChunk *__restrict__ chunks,
-                                                            const uint32_t *__restrict__ ycol,
-                                                            const float *__restrict__ Q1, float *__restrict__ gpart) {
-  typedef float f16x __attribute__((ext_vector_type(16)));
-  __shared__ float red[1024];
-  const GChunk c = chunks[blockIdx.x];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, e = lane & 31;
-  f16x acc;
-#pragma unroll
-  for (int r = 0; r < 16; r++) acc[r] = 0.0f;
-  constexpr int U = 4;
-  for (int64_t p0 = c.b + 2 * w; p0 < c.e; p0 += 8 * U) {
-    float a[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const int64_t p = p0 + 8 * u + hf;
-      a[u] = p < c.e ? Q1[(size_t)ycol[p] * 32 + e] : 0.0f;
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], a[u], acc, 0, 0, 0);
-  }
-  for (int ww = 0; ww < BLOCK / 64; ww++) {
-    if (w == ww)
-#pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const int m = 8 * (r >> 2) + 4 * hf + (r & 3);
-        float &x = red[m * 32 + e];
-        x = (ww == 0 ? 0.0f : x) + acc[r];
-      }
-    __syncthreads();
-  }
-  for (int t = threadIdx.x; t < 1024; t += BLOCK) gpart[(size_t)blockIdx.x * 1024 + t] = red[t];
-}
-
-// G[h] = sum of heavy row h's chunk partials, in chunk order.
-static __global__ __launch_bounds__(BLOCK) void k_gram_rows(const uint32_t *__restrict__ cptr,
-                                                           const float *__restrict__ gpart, float *__restrict__ G) {
-  const uint32_t h = blockIdx.x, c0 = cptr[h], c1 = cptr[h + 1];
-  for (int t = threadIdx.x; t < 1024; t += BLOCK) {
-    float s = 0;
-    for (uint32_t c = c0; c < c1; c++) s += gpart[(size_t)c * 1024 + t];
-    G[(size_t)h * 1024 + t] = s;
-  }
-}
-
-// Hessian-vector row pass + finalisation of a row-complete cross half
-// (hs_cross, ffm.cpp:715-742, then cg 783-809 for the row's column): one row
-// per subgroup; phi_i = x_i p_t(d_i) from the column's finalisation
-// operands; light rows gather their <= HEAVY_POS partner rows in one round,
-// heavy rows multiply by G_i; + w phi QTQ (QTQ in LDS).
-// x M for a global KP x KP matrix, its rows loaded GROUP at a time (bounded
-// register footprint; sg_vecmat issues all KP row loads at once).
-template <typename real, int KP, int GROUP>
-__device__ __forceinline__ vec_t<real> sg_vecmat_g(const vec_t<real> &x, const real *__restrict__ M, int li) {
-  using G = Geo<real, KP>;
-  vec_t<real> t = vzero<real>();
-#pragma unroll 1
-  for (int e0 = 0; e0 < KP; e0 += GROUP) {
-    vec_t<real> mr[GROUP];
-#pragma unroll
-    for (int u = 0; u < GROUP; u++) mr[u] = vld<real>(M + (size_t)(e0 + u) * KP + li * G::VE);
-    sfor<GROUP>([&](auto U) {
-      constexpr int u = decltype(U)::value;
-      // component e0 + u of x lives in lane (e0 + u) / VE of the subgroup
-      const real xe = __shfl(x[(e0 + u) % G::VE], (int)((threadIdx.x & 63) & ~(G::LPR - 1)) + (e0 + u) / G::VE, 64);
-      t += vsplat<real>(xe) * mr[u];
-    });
-  }
-  return t;
-}
-
-template <int KP>
-__global__ __launch_bounds__(BLOCK) void k_hs_cross_rc(uint64_t R, const int64_t *__restrict__ yptr,
-                                                      const uint32_t *__restrict__ xidx,
-                                                      const float *__restrict__ xval,
-                                                      const uint32_t *__restrict__ ycol, const float *__restrict__ Q1,
-                                                      uint64_t q1rows, const float *__restrict__ QTQ,
-                                                      const uint32_t *__restrict__ hidx, const float *__restrict__ Gh,
-                                                      double w, const int *__restrict__ run, const CgState *st, int it,
-                                                      Fin<float> f) {
-  using G = Geo<float, KP>;
-  using PP = PosPass<float, KP, RC_GB>;
-  static_assert(PP::PW >= HEAVY_POS, "a light row is one pass of PW positions");
-  if (run && !*run) return;
-  __shared__ __align__(16) float Qs[KP * KP];
-  for (int t = threadIdx.x; t < KP * KP; t += BLOCK) Qs[t] = QTQ[t];
-  __syncthreads();
-  const BufView qb = buf_view(Q1, q1rows * KP * sizeof(float));
-  const bool upd = it > 1;
-  const float alpha = upd ? (float)st->alpha : 0.0f, beta = upd ? (float)st->beta : 0.0f;
-  WAVE_SETUP
-  const int sg = lane / G::LPR, li = lane % G::LPR;
-  const float cpos = (float)(1 - w);
-  double dsum[3] = {0, 0, 0};
-  for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
-    const uint32_t d = xidx[i];
-    const float x = xval[i];
-    const int64_t b = yptr[i], e = yptr[i + 1];
-    const uint32_t hv = hidx[i];
-    uint32_t jj[PP::UT];
-    if (hv == 0xffffffffu) PP::load_cols(ycol, b, e, li, jj);
-    const FinOps<float> ops = fin_load<float, KP, 1>(f, d, upd, li);
-    vec_t<float> pt = ops.w_or_p;
-    if (upd) pt = (ops.r - vsplat<float>(alpha) * ops.hp) + vsplat<float>(beta) * ops.w_or_p;
-    const vec_t<float> phi = vsplat<float>(x) * pt;
-    vec_t<float> ka = vzero<float>();
-    if (hv != 0xffffffffu) {
-      ka = sg_vecmat_g<float, KP, 8>(phi, Gh + (size_t)hv * KP * KP, li);
-    } else if (e > b) {
-      sfor<PP::PW / PP::GB>([&](auto BT) {  // GB gathers per round
-        constexpr int bt = decltype(BT)::value * PP::GB;
-        if (b + bt >= e) return;
-        vec_t<float> qv[PP::GB];
-        sfor<PP::GB>([&](auto U) {
-          constexpr int u = decltype(U)::value;
-          qv[u] = bld<float>(qb, PP::row_off(PP::template at<bt + u>(jj, li), qb, li));
-        });
-        float dv[PP::GB];
-#pragma unroll
-        for (int u = 0; u < PP::GB; u++) dv[u] = sg_sum<G::LPR>(hsum<float>(phi * qv[u]));
-#pragma unroll
-        for (int u = 0; u < PP::GB; u++) ka += vsplat<float>(dv[u]) * qv[u];
-      });
-    }
-    // (grouped: the fully unrolled sg_vecmat hoists all KP LDS row loads and
-    // doubles the kernel's registers: 256 -> ~130 VGPRs)
-    const vec_t<float> hvec = vsplat<float>(cpos) * ka + vsplat<float>((float)w) * sg_vecmat_g<float, KP, 8>(phi, Qs, li);
-    col_finalize<float, KP, 1>(f, d, vsplat<float>(x) * hvec, alpha, beta, upd, li, dsum, ops);
-  }
-  fin_blocks<float, 1>(f, dsum);
-}
 
 // ------------------------------------------------------ feature pass ---
 // acc_col = sum_{(r, x) in column} x h[r] for every feature column of a field
@@ -1931,9 +1541,7 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
                                                             const uint32_t *__restrict__ ycol,
                                                             real *__restrict__ yt, const real *__restrict__ Q1,
                                                             uint64_t q1rows, const uint32_t *__restrict__ segd,
-                                                            const real *__restrict__ segx,
-                                                            real *__restrict__ yt_other,
-                                                            const uint32_t *__restrict__ perm, real *__restrict__ W,
+                                                            const real *__restrict__ segx, real *__restrict__ W,
                                                             const real *__restrict__ Pd, const CgState *st,
                                                             const real *__restrict__ XSin,
                                                             const real *__restrict__ a1,
@@ -1986,27 +1594,18 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_seg(uint64_t nseg, const
           if ((bt + u) % G::LPR == li) dd[(bt + u) / G::LPR] = d;
         }
       });
-      // each lane owns its positions p0 + li + t*LPR: all loads, then all
-      // stores; yt_other: the same new value also stored at the positive's
-      // place in the other orientation (a plain scattered store, no
-      // read-modify-write: both orientations hold the same base)
+      // each lane owns its positions p0 + li + t*LPR: all loads, then all stores
       real ym[PP::UT];
-      uint32_t pm[PP::UT];
 #pragma unroll
       for (int t = 0; t < PP::UT; t++) {
         const int64_t q = p0 + li + t * G::LPR;
         ym[t] = q < sgm.e ? yt[q] : (real)0;
-        pm[t] = (yt_other && q < sgm.e) ? perm[q] : 0u;
         if (XSin && q < sgm.e) ym[t] -= ai + b1[jj[t]];
       }
 #pragma unroll
       for (int t = 0; t < PP::UT; t++) {
         const int64_t q = p0 + li + t * G::LPR;
-        if (q < sgm.e) {
-          const real v = ym[t] + dd[t];
-          yt[q] = v;
-          if (yt_other) yt_other[pm[t]] = v;
-        }
+        if (q < sgm.e) yt[q] = ym[t] + dd[t];
       }
     }
   }
@@ -2439,16 +2038,19 @@ __global__ __launch_bounds__(BLOCK) void k_scores(uint64_t rows, uint64_t row0, 
 // z[argmax] = MIN_Z (-1000) and first-index tie-break, accumulating hits and
 // DCG/IDCG at the cut-offs 5,10,20,40,80 (validate/prec_k/ndcg,
 // ffm.cpp:982-1128).  One block per row.  out[r] = {ploss, hits[5], ndcg[5]}.
+// forced: the reference's EBUG_nDCG build (ffm.cpp:988-993): after the
+// ploss term the row's scores are replaced by z_j = n - j, j < n.
 static __global__ __launch_bounds__(BLOCK) void k_rank(uint64_t rows, uint64_t row0, uint64_t n, uint64_t max_z,
                                                 double *__restrict__ z, const int64_t *__restrict__ lptr,
                                                 const uint32_t *__restrict__ lcol, const uint8_t *__restrict__ cold,
                                                 uint64_t npop, const double *__restrict__ at,
-                                                double *__restrict__ out) {
+                                                double *__restrict__ out, int forced) {
   const uint64_t r = blockIdx.x;
   const uint64_t i = row0 + r;
   double *zr = z + r * n;
   const int64_t l0 = lptr[i], l1 = lptr[i + 1];
-  const uint64_t zsize = cold[i] ? npop : n;
+  const uint64_t zs0 = cold[i] ? npop : n;  // size of the row's score vector (popularity: #train items)
+  const uint64_t zsize = forced ? n : zs0;     // (resized to n by the forced build)
   const uint64_t mz = max_z < zsize ? max_z : zsize;
   __shared__ double s_val[BLOCK / 64];
   __shared__ uint64_t s_idx[BLOCK / 64];
@@ -2457,12 +2059,16 @@ static __global__ __launch_bounds__(BLOCK) void k_rank(uint64_t rows, uint64_t r
   double pl = 0;
   for (int64_t p = l0 + threadIdx.x; p < l1; p += BLOCK) {
     const uint64_t j = lcol[p];
-    if (j < zsize) {
+    if (j < zs0) {
       const double d = 1 - zr[j] - at[i];
       pl += d * d;
     }
   }
   pl = block_sum(pl);
+  if (forced) {
+    for (uint64_t j = threadIdx.x; j < n; j += BLOCK) zr[j] = (double)(n - j);
+    __syncthreads();
+  }
   const int cut[5] = {5, 10, 20, 40, 80};
   double hits[5] = {0, 0, 0, 0, 0}, dcg[5] = {0, 0, 0, 0, 0}, idcg[5] = {0, 0, 0, 0, 0};
   const uint64_t nlab = (uint64_t)(l1 - l0);

@@ -139,38 +139,7 @@ template <typename real> struct DevSide {
   uint64_t nseg = 0;      // positive segments (kernels.hpp: Seg)
   DevBuf<Seg> segs;
   DevBuf<uint32_t> segptr;
-  // row-complete cross halves (kernels.hpp k_hs_cross_rc): heavy rows (more
-  // than HEAVY_POS positives) and the chunks of their Gram build
-  uint64_t nheavy = 0, nchunk = 0, heavy_pos = 0;
-  DevBuf<uint32_t> hidx;   // R: heavy index or ~0
-  DevBuf<GChunk> chunks;
-  DevBuf<uint32_t> cptr;   // nheavy + 1
-  DevBuf<float> gpart, gram;
 };
-
-// Heavy rows of a side and their Gram chunks (row-complete cross halves).
-template <typename real> static void build_heavy(DevSide<real> &s, const std::vector<int64_t> &yptr) {
-  const uint64_t R = yptr.size() - 1;
-  std::vector<uint32_t> hidx(std::max<uint64_t>(R, 1), 0xffffffffu), cptr{0};
-  std::vector<GChunk> ch;
-  for (uint64_t i = 0; i < R; i++) {
-    const int64_t b = yptr[i], e = yptr[i + 1];
-    if (e - b <= HEAVY_POS) continue;
-    hidx[i] = (uint32_t)s.nheavy++;
-    s.heavy_pos += (uint64_t)(e - b);
-    for (int64_t p = b; p < e; p += GRAM_CHUNK)
-      ch.push_back(GChunk{hidx[i], 0u, p, std::min<int64_t>(e, p + GRAM_CHUNK)});
-    cptr.push_back((uint32_t)ch.size());
-  }
-  s.nchunk = ch.size();
-  s.hidx.upload(hidx);
-  s.chunks.upload(ch.empty() ? std::vector<GChunk>{GChunk{0, 0, 0, 0}} : ch);
-  s.cptr.upload(cptr);
-  if (std::is_same<real, float>::value && s.nheavy) {
-    s.gpart.alloc(s.nchunk * 1024, false);
-    s.gram.alloc(s.nheavy * 1024, false);
-  }
-}
 
 // Split every row's positives into segments of at most `len` (rows without
 // positives still get one, empty, segment for their row-local terms).
@@ -293,12 +262,14 @@ struct ProblemBase {
   virtual void one_epoch() = 0;
   virtual void solve_block(uint32_t f1, uint32_t f2) = 0;
   virtual void cache_sasb() = 0;
-  virtual void validate(ocffm_metrics *m) = 0;
+  virtual void validate(ocffm_metrics *m, bool forced = false, double *per_row_ndcg10 = nullptr) = 0;
   virtual uint64_t get(char what, uint32_t b12, double *out, uint64_t cap) = 0;
   virtual void set(char what, uint32_t b12, const double *in, uint64_t len) = 0;
   virtual void grad(uint32_t f1, uint32_t f2, int half, double *out) = 0;
   virtual void hv(uint32_t f1, uint32_t f2, int half, const double *v, double *out) = 0;
   virtual void save_model(const std::string &path) = 0;
+  virtual void save_binary(const std::string &path) = 0;
+  virtual void load_binary(const std::string &path) = 0;
   virtual void sync() = 0;
   virtual bool has_test() const = 0;
   virtual uint32_t nr_pass() const = 0;
@@ -323,10 +294,6 @@ template <typename real> class Problem final : public ProblemBase {
   Problem(const HostData &U, const HostData *Ut, const HostData &V, const ocffm_param &prm, Comm comm)
       : prm_(prm), comm_(comm), has_test_(Ut != nullptr) {
     HIPCHK(hipSetDevice(prm.device));
-    if (const char *e = std::getenv("OCFFM_SCHED")) {  // host wait policy of event syncs (experiment)
-      const int v = std::atoi(e);
-      (void)hipSetDeviceFlags(v == 1 ? hipDeviceScheduleSpin : v == 2 ? hipDeviceScheduleYield : hipDeviceScheduleBlockingSync);
-    }
     HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     k_ = prm.k;
     kp_ = pad_k(k_);
@@ -346,7 +313,7 @@ template <typename real> class Problem final : public ProblemBase {
     if (const char *e = std::getenv("OCFFM_LOOKAHEAD")) lookahead_ = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("OCFFM_HS_BLOCKS")) hs_blocks_ = (unsigned)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("OCFFM_FEAT_BLOCKS")) feat_blocks_ = (unsigned)std::max(1, std::atoi(e));
-    if (const char *e = std::getenv("OCFFM_FUSE")) fuse_ = std::atoi(e);  // id-field row fusion: 0 off, 1 side, 2 all
+    if (const char *e = std::getenv("OCFFM_FUSE")) fuse_ = std::atoi(e) != 0;  // id-field side Hv rows finalise their column
     if (const char *e = std::getenv("OCFFM_NO_OWNED")) no_owned_ = std::atoi(e) != 0;  // all-reduce every field
     // shard users contiguously
     u0_ = U.m * (uint64_t)comm_.rank / (uint64_t)comm_.nranks;
@@ -384,11 +351,9 @@ template <typename real> class Problem final : public ProblemBase {
     Vd_.alloc(dk);
     Rv_.alloc(dk);
     Hv_.alloc(dk);
-    // h: row or segment partials; the fused id-field passes use it for two
-    // slots per wave-chunk of segments (kernels.hpp chunk_finalize)
+    // h: row or segment partials
     const uint64_t nsegmax = std::max(U_.nseg, V_.nseg);
-    const uint64_t nslots = 2 * ((nsegmax + nsg() - 1) / nsg());
-    h_.alloc(std::max<uint64_t>(std::max(Rmax, std::max(nsegmax, nslots)), 1) * kp_);
+    h_.alloc(std::max<uint64_t>(std::max(Rmax, nsegmax), 1) * kp_);
     if (std::max(U_.R, V_.R) * kp_ * sizeof(real) >= (1ull << 32) - 64)  // partner-row gathers (BufView)
       throw Error(OCFFM_E_DATA, "too many rows per GPU for 32-bit gather offsets; shard over more GPUs");
     if (std::max(U_.npos, V_.npos) * 4 >= (1ull << 32) - 64)  // column reads through a BufView (k_hs_cross_w)
@@ -449,6 +414,10 @@ template <typename real> class Problem final : public ProblemBase {
 
   void init() override {
     ysum_dirty();
+    // a previous epoch that threw inside the cross loop may have left the
+    // block-excluded form on: the base is rebuilt below from scratch
+    excl_ = ExclBase{};
+    lazy_ok_ = false;
     tmark(nullptr);
     const size_t rs = sizeof(real);
     std::vector<double> host;
@@ -470,6 +439,13 @@ template <typename real> class Problem final : public ProblemBase {
       }
     (void)rs;
     (void)host;
+    derive_state();
+  }
+
+  // Everything init() derives from W/H (ffm.cpp:490-511): P/Q are already
+  // UTX'd; the cross-table lists, sa/sb, the side sums a/b (from zero), the
+  // bias sums and y~.  Also the state of a loaded binary snapshot.
+  void derive_state() {
     // cross-table pointer lists used by the gradient / sasb / y~ kernels
     std::vector<real *> tl(4 * std::max<uint32_t>(C_, 1) + 4, nullptr);
     uint32_t c = 0;
@@ -489,6 +465,99 @@ template <typename real> class Problem final : public ProblemBase {
     tmark("init: y~");
     sync();
     inited_ = true;
+  }
+
+  // Binary snapshot in the layout of the reference's save_binary_model
+  // (ffm.cpp:1239-1267, native little-endian): uint32 f, fu, fv, k; uint64
+  // Ds of the user fields, then of the item fields; per block in (f1, f2)
+  // order (cross blocks only under --ns): uint32 index_vec, uint64 |W|,
+  // uint64 |H|, then W and H as doubles, D x k row-major.
+  void save_binary(const std::string &path) override {
+    need_init();
+    std::FILE *fp = std::fopen(path.c_str(), "wb");
+    if (!fp) throw Error(OCFFM_E_IO, "cannot write " + path);
+    bool ok = true;
+    auto put = [&](const void *v, size_t n) { ok = ok && std::fwrite(v, 1, n, fp) == n; };
+    const uint32_t hd[4] = {f_, fu_, fv_, k_};
+    put(hd, sizeof(hd));
+    put(U_.Ds.data(), fu_ * sizeof(uint64_t));
+    put(V_.Ds.data(), fv_ * sizeof(uint64_t));
+    std::vector<double> w, h;
+    for (uint32_t f1 = 0; f1 < f_ && ok; f1++)
+      for (uint32_t f2 = f1; f2 < f_ && ok; f2++) {
+        const uint32_t b12 = block_index(f1, f2, f_);
+        if (!blocks_[b12].used) continue;
+        const uint64_t nw = get('W', b12, nullptr, 0), nh = get('H', b12, nullptr, 0);
+        w.resize(nw);
+        h.resize(nh);
+        get('W', b12, w.data(), nw);
+        get('H', b12, h.data(), nh);
+        put(&b12, sizeof(b12));
+        put(&nw, sizeof(nw));
+        put(&nh, sizeof(nh));
+        put(w.data(), nw * sizeof(double));
+        put(h.data(), nh * sizeof(double));
+      }
+    ok = (std::fclose(fp) == 0) && ok;
+    if (!ok) throw Error(OCFFM_E_IO, "write failed: " + path);
+  }
+
+  // What the reference's load_binary_model (ffm.cpp:1269-1301) was written
+  // to do (it opens an ofstream and writes instead): read the layout above,
+  // check it against this problem, restore W/H and re-derive P, Q, sa/sb,
+  // a/b and y~ as init does.  The result is the state init() would reach if
+  // its draw had produced these tables.
+  void load_binary(const std::string &path) override {
+    std::FILE *fp = std::fopen(path.c_str(), "rb");
+    if (!fp) throw Error(OCFFM_E_IO, "cannot read " + path);
+    std::unique_ptr<std::FILE, int (*)(std::FILE *)> guard(fp, &std::fclose);
+    auto get_ = [&](void *v, size_t n) {
+      if (std::fread(v, 1, n, fp) != n) throw Error(OCFFM_E_DATA, "truncated binary model: " + path);
+    };
+    uint32_t hd[4];
+    get_(hd, sizeof(hd));
+    if (hd[0] != f_ || hd[1] != fu_ || hd[2] != fv_ || hd[3] != k_)
+      throw Error(OCFFM_E_DATA, "binary model: f/fu/fv/k differ from this problem");
+    std::vector<uint64_t> du(fu_), dv(fv_);
+    get_(du.data(), fu_ * sizeof(uint64_t));
+    get_(dv.data(), fv_ * sizeof(uint64_t));
+    if (du != U_.Ds || dv != V_.Ds) throw Error(OCFFM_E_DATA, "binary model: field sizes differ from this problem");
+    ysum_dirty();
+    excl_ = ExclBase{};
+    lazy_ok_ = false;
+    std::vector<double> w;
+    for (uint32_t f1 = 0; f1 < f_; f1++)
+      for (uint32_t f2 = f1; f2 < f_; f2++) {
+        const uint32_t b12 = block_index(f1, f2, f_);
+        if (!blocks_[b12].used) continue;
+        uint32_t idx;
+        uint64_t nw, nh;
+        get_(&idx, sizeof(idx));
+        get_(&nw, sizeof(nw));
+        get_(&nh, sizeof(nh));
+        DevSide<real> &s1 = side(f1), &s2 = side(f2);
+        const uint64_t D1 = s1.Ds[fidx(f1)], D2 = s2.Ds[fidx(f2)];
+        if (idx != b12 || nw != D1 * k_ || nh != D2 * k_) throw Error(OCFFM_E_DATA, "binary model: block table differs");
+        for (int t = 0; t < 2; t++) {
+          const uint64_t D = t == 0 ? D1 : D2;
+          w.resize(D * k_);
+          get_(w.data(), w.size() * sizeof(double));
+          DevBuf<real> &dst = t == 0 ? W_[b12] : H_[b12];
+          if (!dst.p) dst.alloc(D * kp_);
+          std::vector<real> pad(D * kp_, (real)0);
+          for (uint64_t rr = 0; rr < D; rr++)
+            for (uint32_t cc = 0; cc < k_; cc++) pad[rr * kp_ + cc] = (real)w[rr * k_ + cc];
+          HIPCHK(hipMemcpy(dst.p, pad.data(), pad.size() * sizeof(real), hipMemcpyHostToDevice));
+        }
+        if (!P_[b12].p) P_[b12].alloc(std::max<uint64_t>(s1.R, 1) * kp_);
+        if (!Q_[b12].p) Q_[b12].alloc(std::max<uint64_t>(s2.R, 1) * kp_);
+        utx(s1, fidx(f1), W_[b12].p, P_[b12].p);
+        utx(s2, fidx(f2), H_[b12].p, Q_[b12].p);
+      }
+    HIPCHK(hipMemsetAsync(U_.bias.p, 0, U_.bias.bytes(), stream_));
+    HIPCHK(hipMemsetAsync(V_.bias.p, 0, V_.bias.bytes(), stream_));
+    owned_stale_ = false;
+    derive_state();
   }
 
   // ------------------------------------------------------------ epoch
@@ -605,7 +674,10 @@ template <typename real> class Problem final : public ProblemBase {
   }
 
   // ------------------------------------------------------- validation
-  void validate(ocffm_metrics *out) override {
+  // forced: the reference's nDCG debug build (EBUG_nDCG, ffm.cpp:988-993):
+  // after the ploss term every row's scores become z_j = n - j; per_row
+  // (optional, this rank's test rows): nDCG@10 of each row (ffm.cpp:1126).
+  void validate(ocffm_metrics *out, bool forced = false, double *per_row = nullptr) override {
     need_init();
     sync_owned();
     static const uint32_t cuts[5] = {5, 10, 20, 40, 80};
@@ -662,7 +734,7 @@ template <typename real> class Problem final : public ProblemBase {
                                                      popular_.p, npop_, z.p);
       });
       launch(k_rank, (unsigned)rows, BLOCK, 0, rows, r0, n_, max_z, z.p, T_.yptr.p, T_.ycol.p, cold_.p, npop_,
-                                                    at_double(at, mt), rowout.p + r0 * 11);
+             at_double(at, mt), rowout.p + r0 * 11, (int)forced);
       HIPCHK(hipGetLastError());
     }
     std::vector<double> ro(mt * 11);
@@ -671,6 +743,8 @@ template <typename real> class Problem final : public ProblemBase {
     std::vector<double> tot(11, 0.0);
     for (uint64_t i = 0; i < mt; i++)
       for (int x = 0; x < 11; x++) tot[x] += ro[i * 11 + x];
+    if (per_row)
+      for (uint64_t i = 0; i < mt; i++) per_row[i] = ro[i * 11 + 7];
     allreduce_host(tot.data(), tot.size());
     const double mt_glob = (double)T_.R_glob;
     out->loss = std::sqrt(tot[0] / mt_glob);
@@ -747,6 +821,7 @@ template <typename real> class Problem final : public ProblemBase {
   void set(char what, uint32_t b12, const double *in, uint64_t len) override {
     ysum_dirty();
     need_init();
+    flush_base();  // restore the full base while P/Q still match it
     if (b12 >= blocks_.size() || !blocks_[b12].used) throw Error(OCFFM_E_ARG, "block not in the model");
     const Block &b = blocks_[b12];
     const bool isW = what == 'W';
@@ -784,7 +859,6 @@ template <typename real> class Problem final : public ProblemBase {
       aggregates(hc.partner->R, (int)C_, partner_tabs(hc), hc.Q1, nullptr, M_.p);
       const uint32_t c0 = cross_slot(std::min(hc.fl, hc.fo), std::max(hc.fl, hc.fo));
       qtq_ = M_.p + (size_t)c0 * kp_ * kp_;
-      heavy_grams(hc);
     }
     col_grams(hc);
     // force iteration 1 to run
@@ -952,7 +1026,6 @@ template <typename real> class Problem final : public ProblemBase {
     for (uint64_t p = pb; p < pe; p++) ycol[p - pb] = (uint32_t)U.ycol[p];
     U_.npos = pe - pb;
     build_segments(U_, yptr, seg_len_, nsg());
-    build_heavy(U_, yptr);
     U_.yptr.upload(yptr);
     U_.ycol.upload(ycol);
     U_.yt.alloc(std::max<uint64_t>(U_.npos, 1));
@@ -993,7 +1066,6 @@ template <typename real> class Problem final : public ProblemBase {
       gn1_ = (double)U.m;
     }
     build_segments(V_, vptr, seg_len_, nsg());
-    build_heavy(V_, vptr);
     V_.yptr.upload(vptr);
     V_.ycol.upload(vcol);
     V_.yt.alloc(std::max<uint64_t>(np, 1));
@@ -1382,7 +1454,6 @@ template <typename real> class Problem final : public ProblemBase {
   // gd_side / gd_cross (ffm.cpp:537-703) -> G, and the CG start vectors.
   void gradient(HalfCtx &h) {
     DevSide<real> &own = *h.own;
-    const bool fz_ = fused_rows(h, false);
     if (!(lazy_ok_ && h.cross)) flush_base();  // this half reads (or updates) the full base
     if (h.cross) ysum_dirty();                   // (entering a block rewrites the stored base)
     with_kp(kp_, [&](auto K) {
@@ -1416,7 +1487,7 @@ template <typename real> class Problem final : public ProblemBase {
         if (enter) bytes += (double)own.npos * rs + (dxs ? (double)ps.R * KP * rs : 0);
         // inside the block (BM_IN): read the stored value through perm from
         // the orientation the entering pass wrote (no refresh in between)
-        const bool via = ytvia_ && cur && !enter && !lazy_scatter_;
+        const bool via = ytvia_ && cur && !enter;
         // T_i = sum_c P_c[i] M_c on MFMA ahead of the pass (k_rows_T32)
         const bool tp = tpre(own.R);
         if (tp) {
@@ -1440,17 +1511,16 @@ template <typename real> class Problem final : public ProblemBase {
             });
           }
         }
-        auto go2 = [&](auto fz, auto ml, auto bm) {
-          constexpr bool FZ = decltype(fz)::value, ML = decltype(ml)::value;
+        auto go2 = [&](auto ml, auto bm) {
+          constexpr bool ML = decltype(ml)::value;
           constexpr int BM = decltype(bm)::value;
           auto go3 = [&](auto tpc) {
             constexpr bool TP = decltype(tpc)::value;
-            launch(k_gd_cross_seg<real, KP, ML, FZ, BM, TP>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : gd_blocks_), BLOCK,
+            launch(k_gd_cross_seg<real, KP, ML, BM, TP>, grid_for(own.nseg, 4 * Gm::NSG, gd_blocks_), BLOCK,
                 TP ? 0 : (ML ? msz : 0), own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
                 (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, h.partner->bias.p, w_,
-                r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, (uint64_t)h.partner->R, fin, (const uint32_t *)own.segptr.p,
-                cur, drow, dxs, (enter && lazy_scatter_) ? h.partner->yt.p : (real *)nullptr,
-                (const uint32_t *)own.perm.p, TP ? (const real *)Tpre_.p : (const real *)nullptr,
+                r_, h_.p, (uint64_t)h.partner->R, cur, drow, dxs, (const uint32_t *)own.perm.p,
+                TP ? (const real *)Tpre_.p : (const real *)nullptr,
                 via ? (const real *)h.partner->yt.p : (const real *)nullptr);
           };
           if constexpr (std::is_same<real, float>::value && KP == 32 && ML) {
@@ -1461,23 +1531,18 @@ template <typename real> class Problem final : public ProblemBase {
           }
           go3(std::false_type());
         };
-        auto go = [&](auto fz, auto ml) {
-          if (!cur) go2(fz, ml, std::integral_constant<int, BM_FULL>());
-          else if (enter) go2(fz, ml, std::integral_constant<int, BM_ENTER>());
-          else go2(fz, ml, std::integral_constant<int, BM_IN>());
+        auto go = [&](auto ml) {
+          if (!cur) go2(ml, std::integral_constant<int, BM_FULL>());
+          else if (enter) go2(ml, std::integral_constant<int, BM_ENTER>());
+          else go2(ml, std::integral_constant<int, BM_IN>());
         };
-        prof_launch(fz_ ? "gd_cross_fused" : "gd_cross_row", bytes, [&] {
-          if (fz_) {
-            if (lds) go(std::true_type(), std::true_type());
-            else go(std::true_type(), std::false_type());
-          } else {
-            if (lds) go(std::false_type(), std::true_type());
-            else go(std::false_type(), std::false_type());
-          }
+        prof_launch("gd_cross_row", bytes, [&] {
+          if (lds) go(std::true_type());
+          else go(std::false_type());
         });
         // the other orientation: refreshed here, or read through perm by the
         // block's second half (ytvia_; flush_base refreshes it after the loop)
-        if (enter && !lazy_scatter_ && !ytvia_) refresh_other(own, *h.partner);
+        if (enter && !ytvia_) refresh_other(own, *h.partner);
         // QTQ for CG = M of this block (M_ is not rewritten before the half ends)
         const uint32_t c0 = cross_slot(std::min(h.fl, h.fo), std::max(h.fl, h.fo));
         qtq_ = M_.p + (size_t)c0 * KP * KP;
@@ -1497,20 +1562,16 @@ template <typename real> class Problem final : public ProblemBase {
                    own.ycol.p, (const real *)own.yt.p, (const real *)other.bias.p, (uint64_t)other.R, ysum_.p);
           });
           ysum_ok_[ys] = true;
+          ysum_ok_[1 - ys] = false;  // one buffer for both sides: the other side's sums are gone
         }
         const real *ysum = ysum_on_ ? (const real *)ysum_.p : nullptr;
-        auto go = [&](auto fz) {
-          constexpr bool FZ = decltype(fz)::value;
-          launch(k_gd_side_seg<real, KP, FZ>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : 4096u), BLOCK, 0,
-              own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, own.bias.p, other.bias.p, own.s.p, bsum_.p + (h.user ? 1 : 0),
-              n1, w_, r_, h_.p, F.xptr.p, F.xidx.p, F.xval.p, (uint64_t)other.R, fin, (const uint32_t *)own.segptr.p, ysum);
-        };
-        prof_launch(fz_ ? "gd_side_fused" : "gd_side_row", bytes, [&] {
-          if (fz_) go(std::true_type());
-          else go(std::false_type());
+        prof_launch("gd_side_row", bytes, [&] {
+          launch(k_gd_side_seg<real, KP>, grid_for(own.nseg, 4 * Gm::NSG), BLOCK, 0, own.nseg, own.segs.p, own.ycol.p,
+                 own.yt.p, h.Q1, own.bias.p, other.bias.p, own.s.p, bsum_.p + (h.user ? 1 : 0), n1, w_, r_, h_.p,
+                 (uint64_t)other.R, ysum);
         });
       }
-      if (!fz_) feature_pass(h, 0, true);
+      feature_pass(h, 0, true);
     });
   }
 
@@ -1537,7 +1598,7 @@ template <typename real> class Problem final : public ProblemBase {
                   [&] {
                     launch(k_update_cross_seg<real, KP>, grid_for(own.nseg, 4 * Gm::NSG), BLOCK, 0, own.nseg,
                            own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, (const real *)S_.p, (real *)nullptr, own.ycol.p,
-                           own.yt.p, Q1, (uint64_t)other.R, F.segd.p, F.segx.p, (real *)nullptr, own.perm.p,
+                           own.yt.p, Q1, (uint64_t)other.R, F.segd.p, F.segx.p,
                            (real *)nullptr, (const real *)nullptr, (const CgState *)st_.p, P1,
                            (const real *)U_.bias.p, (const real *)V_.bias.p, (const int *)nullptr);
                   });
@@ -1577,20 +1638,6 @@ template <typename real> class Problem final : public ProblemBase {
     f.tw = w_;
     return f;
   }
-  // id-like field on one GPU: the row pass finalises its feature column.
-  // The heavy rows' Grams G_i = sum_j q_j q_j^T of a row-complete half (its
-  // partner rows q_j are fixed for the whole CG solve).
-  void heavy_grams(const HalfCtx &h) {
-    if (!row_complete(h) || !h.own->nheavy) return;
-    DevSide<real> &own = *h.own;
-    prof_launch("heavy_gram", (double)own.heavy_pos * (4 + 128) + own.nchunk * 4096.0 * 2, [&] {
-      launch(k_pos_gram32, (unsigned)own.nchunk, BLOCK, 0, (const GChunk *)own.chunks.p, (const uint32_t *)own.ycol.p,
-             (const float *)h.Q1, (float *)own.gpart.p);
-      launch(k_gram_rows, (unsigned)own.nheavy, BLOCK, 0, (const uint32_t *)own.cptr.p, (const float *)own.gpart.p,
-             (float *)own.gram.p);
-    });
-  }
-
   // Gram chunks of a one-node-per-row field (build_csc's column order): each
   // column in chunks of at most cgram_rows rows (one LDS stage: larger
   // OCFFM_CGRAM_CHUNK values are capped there); empty columns get one empty
@@ -1618,16 +1665,6 @@ template <typename real> class Problem final : public ProblemBase {
     F.gchunks.upload(chunks);
     if (cgram32() && !sums.empty()) F.gsums.upload(sums);
     F.gslots = slots;
-  }
-
-  // A Gram side half with at most one column per subgroup of one
-  // CGS_THREADS block solves its whole CG in one launch (k_cg_gram_small).
-  // Opt-in (OCFFM_CGSMALL=1): measured slower at kkbox shape (DESIGN §7:
-  // 41 us per genre half against ~3 launches of 7.5 us; one CU streams the
-  // Grams and waits out each step's chain alone).
-  bool cgsmall_on_ = std::getenv("OCFFM_CGSMALL") && std::atoi(std::getenv("OCFFM_CGSMALL")) != 0;
-  bool cg_small(const HalfCtx &h) const {
-    return cgsmall_on_ && cgram(h) && !comm_.active() && h.D <= (uint64_t)(CGS_THREADS / 64) * nsg();
   }
 
   // fp32 at KP = 32: the Grams are built on MFMA (kernels.hpp k_col_gram32)
@@ -1681,15 +1718,6 @@ template <typename real> class Problem final : public ProblemBase {
     });
   }
 
-  // Row-complete cross half (kernels.hpp k_hs_cross_rc): fp32 at KP = 32,
-  // one GPU, id-like field, and the heavy rows' Grams cheap to build (at most
-  // a quarter of the side's positives in heavy rows: the items, whose heavy
-  // rows are the Pareto head; not the users, most of whom are heavy).
-  bool row_complete(const HalfCtx &h) const {
-    return std::is_same<real, float>::value && kp_ == 32 && h.cross && h.F->idlike && !comm_.active() && rc_ &&
-           h.own->heavy_pos * 4 <= h.own->npos;
-  }
-
   // Column tau: the w phi_i QTQ term of a cross half's Hessian-vector rows,
   // for a one-node-per-row field, is w (sum_{i in col d} x_i^2) p_d QTQ per
   // column, added by the feature pass (k_feat TAU) instead of per row by
@@ -1700,21 +1728,16 @@ template <typename real> class Problem final : public ProblemBase {
   // sum x^2, a partial over local rows on the user halves).
   static constexpr size_t COLTAU_LDS = 32 * 1024;
   bool coltau(const HalfCtx &h) const {
-    return coltau_on_ && h.cross && h.F->one && !fused_rows(h, true) && !row_complete(h) &&
+    return coltau_on_ && h.cross && h.F->one &&
            (size_t)kp_ * kp_ * sizeof(real) <= COLTAU_LDS;
   }
 
-  // fuse_ 3: both row passes of side halves (gradient and Hessian-vector).
-  // fuse_ 1: the Hessian-vector pass of side halves only (one row = one
-  // feature, no partial sums); 2: every row pass of an id-like field (the
-  // gradient passes and the cross halves walk positive segments: a row's
-  // segments meet in the wave's LDS, or through ordered chunk slots and a
-  // last-arriver sum when the row spans several chunks, kernels.hpp
-  // chunk_finalize).
-  bool fused_rows(const HalfCtx &h, bool hv) const {
-    const bool side = !h.cross;
-    return h.F->idlike && (!comm_.active() || (hv && repl(h))) &&
-           (fuse_ == 2 || (side && (fuse_ == 3 || (fuse_ == 1 && hv))));
+  // The Hessian-vector row pass of an id-like field's side half finalises
+  // its row's feature column itself (one row = one feature, no partial sums;
+  // OCFFM_FUSE=0: a separate feature pass).  Cross halves and the gradient
+  // passes walk positive segments, whose sums a feature pass assembles.
+  bool fused_rows(const HalfCtx &h) const {
+    return fuse_ && h.F->idlike && !h.cross && (!comm_.active() || repl(h));
   }
 
   // Several ranks, id-like field (replicated rows, e.g. items; never an owned
@@ -1824,22 +1847,6 @@ template <typename real> class Problem final : public ProblemBase {
   void hv_pass(HalfCtx &h, int it) {
     DevSide<real> &own = *h.own;
     const int *run = &st_.p->run[it];
-    if (row_complete(h)) {
-      if constexpr (std::is_same<real, float>::value) {
-        DevField<real> &F = *h.F;
-        const Fin<real> fin = make_fin(h, it);
-        const double rs = sizeof(real);
-        const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)own.npos * 4 +
-                             (double)h.partner->R * 32 * rs + (double)own.nheavy * 4096 + (double)F.D * 32 * rs * 8;
-        prof_launch("hs_cross_rc", bytes, [&] {
-          launch(k_hs_cross_rc<32>, grid_for(own.R, 4 * Geo<float, 32>::NSG, 2048), BLOCK, 0, (uint64_t)own.R,
-                 (const int64_t *)own.yptr.p, (const uint32_t *)F.xidx.p, (const float *)F.xval.p,
-                 (const uint32_t *)own.ycol.p, (const float *)h.Q1, (uint64_t)h.partner->R, (const float *)qtq_,
-                 (const uint32_t *)own.hidx.p, (const float *)own.gram.p, w_, run, (const CgState *)st_.p, it, fin);
-        });
-      }
-      return;
-    }
     if (cgram(h)) {
       with_kp(kp_, [&](auto K) {
         constexpr int KP = decltype(K)::value;
@@ -1864,7 +1871,7 @@ template <typename real> class Problem final : public ProblemBase {
       });
       return;
     }
-    const bool fz_ = fused_rows(h, true);
+    const bool fz_ = fused_rows(h);
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
       using Gm = Geo<real, KP>;
@@ -1878,20 +1885,16 @@ template <typename real> class Problem final : public ProblemBase {
           const size_t smem = lds ? qsz : 0;
           const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
                                (double)own.npos * 4 + (double)h.partner->R * KP * rs + (double)own.R * KP * rs;
-          auto go = [&](auto fz, auto ml) {
-            constexpr bool FZ = decltype(fz)::value, ML = decltype(ml)::value;
-            launch(k_hs_cross_seg<real, KP, ML, FZ>, grid_for(own.nseg, 4 * Gm::NSG, FZ ? 2048u : hs_blocks_), BLOCK, smem, own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p,
-                                                         own.ycol.p, h.Q1, (uint64_t)h.partner->R, coltau(h) ? (const real *)nullptr : (const real *)qtq_, w_, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
-                                                         F.segd.p, F.segx.p, fin, (const uint32_t *)own.segptr.p);
+          auto go = [&](auto ml) {
+            constexpr bool ML = decltype(ml)::value;
+            launch(k_hs_cross_seg<real, KP, ML>, grid_for(own.nseg, 4 * Gm::NSG, hs_blocks_), BLOCK, smem, own.nseg,
+                   own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.ycol.p, h.Q1, (uint64_t)h.partner->R,
+                   coltau(h) ? (const real *)nullptr : (const real *)qtq_, w_, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
+                   F.segd.p, F.segx.p);
           };
-          prof_launch(fz_ ? "hs_cross_fused" : "hs_cross_row", bytes, [&] {
-            if (fz_) {
-              if (lds) go(std::true_type(), std::true_type());
-              else go(std::true_type(), std::false_type());
-            } else {
-              if (lds) go(std::false_type(), std::true_type());
-              else go(std::false_type(), std::false_type());
-            }
+          prof_launch("hs_cross_row", bytes, [&] {
+            if (lds) go(std::true_type());
+            else go(std::false_type());
           });
         } else {
           const double n1 = hess_n1(h);
@@ -1929,7 +1932,6 @@ template <typename real> class Problem final : public ProblemBase {
     std::memset(run_host_, 0, sizeof(int) * (MAXCG + 2));
     std::atomic_thread_fence(std::memory_order_seq_cst);
     gradient(h);
-    heavy_grams(h);
     col_grams(h);
     // CG with `lookahead_` iterations in flight (see file header): iteration
     // it is enqueued before the host waits for iteration it-L's verdict, so
@@ -1964,23 +1966,6 @@ template <typename real> class Problem final : public ProblemBase {
                                                 : 0;
     bool queued = false;
     const size_t pend0 = pending_.size();
-    if (cg_small(h)) {
-      // the whole solve in one launch (k_cg_gram_small), the update queued
-      // right behind it; the verdicts are read for the log only
-      prof_tag_ = 1;
-      with_kp(kp_, [&](auto K) {
-        constexpr int KP = decltype(K)::value;
-        // (the bytes of one CG step: the launch runs all of them)
-        prof_launch("cg_gram_small", (double)h.D * KP * KP * sizeof(real) + (double)h.D * KP * sizeof(real) * 9, [&] {
-          launch(k_cg_gram_small<real, KP>, 1, CGS_THREADS, 0, (uint64_t)h.D, (const real *)h.F->gram.p,
-                 make_fin(h, 1));
-        });
-      });
-      prof_tag_ = 0;
-      finish_half(h, nullptr);
-      queued = true;
-      examine(MAXCG);
-    }
     for (int it = 1; it <= MAXCG && !done && !queued; it++) {
       prof_tag_ = it;
       hv_pass(h, it);
@@ -2062,11 +2047,11 @@ template <typename real> class Problem final : public ProblemBase {
         prof_launch("update_cross_row", bytes, [&] {
           launch(k_update_cross_seg<real, KP>, grid_for(own.nseg, 4 * Gm::NSG), BLOCK, 0,
               own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, own.ycol.p, own.yt.p, h.Q1,
-              (uint64_t)other.R, F.segd.p, F.segx.p, scatter_ ? other.yt.p : nullptr, own.perm.p, Wf,
+              (uint64_t)other.R, F.segd.p, F.segx.p, Wf,
               (const real *)Vd_.p, (const CgState *)st_.p, (const real *)nullptr, (const real *)nullptr,
               (const real *)nullptr, skip);
         });
-        if (!scatter_) refresh_other(own, other, skip);  // gather the other orientation instead
+        refresh_other(own, other, skip);  // the other orientation by a gather through perm
       } else {
         DevSide<real> &other = h.user ? V_ : U_;
         const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
@@ -2146,13 +2131,7 @@ template <typename real> class Problem final : public ProblemBase {
   void ysum_dirty() { ysum_ok_[0] = ysum_ok_[1] = false; }
   // OCFFM_SPEC_FIXED=n (tests): predict n for every half (hits and misses of every kind)
   int spec_fixed_ = std::getenv("OCFFM_SPEC_FIXED") ? std::atoi(std::getenv("OCFFM_SPEC_FIXED")) : 0;
-  int fuse_ = 1;
-  // OCFFM_RC=1: row-complete id-field cross halves (k_hs_cross_rc).  Correct
-  // (tests) but measured slower at kkbox shape: 57 us per CG step against
-  // 25 + 15 us for the segment row pass + feature pass (its light rows take
-  // four gather rounds at the register budget of 3 waves/SIMD, where the
-  // segment pass issues all 32 gathers at once at 4 waves/SIMD).
-  bool rc_ = std::getenv("OCFFM_RC") != nullptr;
+  bool fuse_ = true;
   // OCFFM_COLTAU=0: the tau term of cross Hessian-vector rows per row (k_hs_cross_seg)
   bool coltau_on_ = !std::getenv("OCFFM_COLTAU") || std::atoi(std::getenv("OCFFM_COLTAU")) != 0;
   // OCFFM_NO_FOLD=1: k_apply as its own launch on id-like fields too
@@ -2165,11 +2144,6 @@ template <typename real> class Problem final : public ProblemBase {
   // OCFFM_CGRAM_CHUNK: rows per k_col_gram block, capped at one LDS stage
   // (cgram_rows: 256 rows at k = 32 fp32)
   uint64_t cgram_chunk_ = std::getenv("OCFFM_CGRAM_CHUNK") ? std::max(1, std::atoi(std::getenv("OCFFM_CGRAM_CHUNK"))) : 128;
-  // OCFFM_SCATTER=1: the cross update also writes the other orientation of
-  // base by scattered 4-B stores instead of the gather kernel k_gather_pos
-  // (measured 2 % slower per epoch: the scattered partial-line writes cost
-  // more than the coalesced gather pass)
-  bool scatter_ = std::getenv("OCFFM_SCATTER") != nullptr;
   bool no_mfma_ = std::getenv("OCFFM_NO_MFMA") != nullptr;  // Grams on the VALU kernel instead
   uint64_t gram_blocks_ = std::getenv("OCFFM_GRAM_BLOCKS") ? std::strtoull(std::getenv("OCFFM_GRAM_BLOCKS"), nullptr, 10) : 512;
   bool no_owned_ = false;
@@ -2193,9 +2167,6 @@ template <typename real> class Problem final : public ProblemBase {
   bool lazy_ok_ = false;  // set by one_epoch around its cross halves
   // OCFFM_LAZY_BASE=0: every cross update applies its base change at once
   bool lazy_base_ = !std::getenv("OCFFM_LAZY_BASE") || std::atoi(std::getenv("OCFFM_LAZY_BASE")) != 0;
-  // OCFFM_LAZY_SCATTER=1: the gradient pass entering a block also stores the
-  // other orientation (scattered 4-B stores) instead of a refresh gather after it
-  bool lazy_scatter_ = std::getenv("OCFFM_LAZY_SCATTER") && std::atoi(std::getenv("OCFFM_LAZY_SCATTER")) != 0;
   // grid cap of the cross gradient pass (each block stages the C aggregates M in LDS)
   unsigned gd_blocks_ = std::getenv("OCFFM_GD_BLOCKS") ? (unsigned)std::atoi(std::getenv("OCFFM_GD_BLOCKS")) : 2048u;
   bool want_g_ = false;  // grad(): the gradient finalisation also stores G
@@ -2420,6 +2391,11 @@ int ocffm_problem_solve_block(ocffm_problem *prob, uint32_t f1, uint32_t f2) {
 }
 int ocffm_problem_cache_sasb(ocffm_problem *prob) { PROB_CALL(prob->p->cache_sasb()); }
 int ocffm_problem_validate(ocffm_problem *prob, ocffm_metrics *m) { PROB_CALL(prob->p->validate(m)); }
+int ocffm_problem_validate_forced(ocffm_problem *prob, ocffm_metrics *m, double *per_row_ndcg10) {
+  PROB_CALL(prob->p->validate(m, true, per_row_ndcg10));
+}
+int ocffm_problem_save_binary(ocffm_problem *prob, const char *path) { PROB_CALL(prob->p->save_binary(path)); }
+int ocffm_problem_load_binary(ocffm_problem *prob, const char *path) { PROB_CALL(prob->p->load_binary(path)); }
 
 int ocffm_print_header(void) {
   std::cout << "iter";

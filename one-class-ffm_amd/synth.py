@@ -204,6 +204,37 @@ def kkbox(seed: int = 7, m: int = 30755, n: int = 100000, mean: float = 120.0,
                    params=dict(k=32, t=20, l=4.0, w=0.0078125, r=-1.0))
 
 
+def cfg5(m: int = 2_000_000, n: int = 250_000, fu: int = 39, d_user: int = 250_000, k: int = 64,
+         mean_pos: float = 4.0, seed: int = 5, test_rows: int = 0, name: str = "cfg5") -> Dataset:
+    """BASELINE configs[4] as restated in SURVEY §8d (one GPU's row shard of
+    the 100 M-row run): --ns, fu = 39 user fields of D = 250,000 features
+    each (one node per row, value 1), fv = 1 item field (the item id, D = n),
+    ~4 positives per row, k = 64.  Feature ids are half uniform, half
+    Lomax(1.2)-skewed (a popular head per field, like real CTR fields); the
+    positives are drawn like kkbox's (uniform w.p. 1/2, else the Pareto head)."""
+    rng = np.random.default_rng(seed)
+    ptr, col = _positives(rng, m, n, mean_pos)
+
+    def user_fields(count):
+        ids = np.empty((count, fu), dtype=np.uint64)
+        for f in range(fu):
+            uni = rng.integers(0, d_user, size=count)
+            par = np.minimum(np.floor(rng.pareto(1.2, size=count)), d_user - 1).astype(np.int64)
+            # a field-specific permutation keeps the heads of different fields apart
+            par = (par * 7919 + f * 104729) % d_user
+            ids[:, f] = np.where(rng.random(count) < 0.5, uni, par)
+        return [(f, ids[:, f:f + 1], np.ones((count, 1))) for f in range(fu)]
+
+    train = _fast_rows(m, user_fields(m), ptr, col)
+    item = _fast_rows(n, [(0, np.arange(n, dtype=np.uint64)[:, None], np.ones((n, 1)))])
+    test = None
+    if test_rows:
+        tptr, tcol = _positives(rng, test_rows, n, mean_pos)
+        test = _fast_rows(test_rows, user_fields(test_rows), tptr, tcol)
+    return Dataset(name, train, item, test, k=k,
+                   params=dict(k=k, t=20, l=4.0, w=0.0078125, r=-1.0))
+
+
 def kkbox_small(seed: int = 11) -> Dataset:
     """A kkbox-shaped input small enough for the fp64 oracle in a few seconds."""
     return kkbox(seed=seed, m=2000, n=3000, mean=30.0, name="kkbox_small")

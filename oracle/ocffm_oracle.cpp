@@ -933,6 +933,27 @@ struct Problem {
         block(H[b12], r2, 'H', fi, fj);
       }
   }
+
+  // ffm.cpp:1239-1267 — binary model: u32 f, fu, fv, k; u64 user Ds, item
+  // Ds; per used block u32 index_vec, u64 |W|, u64 |H|, W and H as doubles.
+  void save_binary(const std::string &path) const {
+    std::ofstream o(path, std::ios::binary | std::ios::trunc);
+    const u32 hd[4] = {f, fu, fv, k};
+    o.write(reinterpret_cast<const char *>(hd), sizeof(hd));
+    o.write(reinterpret_cast<const char *>(U->Ds.data()), sizeof(u64) * fu);
+    o.write(reinterpret_cast<const char *>(V->Ds.data()), sizeof(u64) * fv);
+    for (u32 fi = 0; fi < f; fi++)
+      for (u32 fj = fi; fj < f; fj++) {
+        if (!block_used(fi, fj)) continue;
+        const u32 b12 = block_index(fi, fj, f);
+        const u64 nw = W[b12].size(), nh = H[b12].size();
+        o.write(reinterpret_cast<const char *>(&b12), sizeof(b12));
+        o.write(reinterpret_cast<const char *>(&nw), sizeof(nw));
+        o.write(reinterpret_cast<const char *>(&nh), sizeof(nh));
+        o.write(reinterpret_cast<const char *>(W[b12].data()), sizeof(double) * nw);
+        o.write(reinterpret_cast<const char *>(H[b12].data()), sizeof(double) * nh);
+      }
+  }
 };
 
 }  // namespace orc
@@ -1155,6 +1176,7 @@ void orc_times(double *out, int reset) {
 }
 
 void orc_save_model(void *c, const char *path) { ((OrcCtx *)c)->prob.save_model(path); }
+void orc_save_binary(void *c, const char *path) { ((OrcCtx *)c)->prob.save_binary(path); }
 
 // Wall-clock seconds of `epochs` calls to one_epoch (the CPU baseline).
 double orc_time_epochs(void *c, uint32_t epochs) {

@@ -61,6 +61,7 @@ def lib():
         L.orc_grad.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, _f64p]
         L.orc_hv.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, _f64p, _f64p]
         L.orc_save_model.argtypes = [C.c_void_p, C.c_char_p]
+        L.orc_save_binary.argtypes = [C.c_void_p, C.c_char_p]
         L.orc_times.argtypes = [C.c_void_p, C.c_int]
         L.orc_time_epochs.restype = C.c_double
         L.orc_time_epochs.argtypes = [C.c_void_p, C.c_uint32]
@@ -191,6 +192,9 @@ class Oracle:
 
     def save_model(self, path):
         lib().orc_save_model(self.h, path.encode())
+
+    def save_binary(self, path):
+        lib().orc_save_binary(self.h, path.encode())
 
     def time_epochs(self, epochs, threads=None):
         if threads is not None:

@@ -159,6 +159,14 @@ def test_sharded_decomposition_gloo():
 def _dist_dataset(name):
     if name == "tiny":
         return synth.tiny(seed=8)
+    if name == "lowcard":
+        # one-node low-cardinality fields on both sides (user field 1: D = 6,
+        # item field 1: D = 5): with OCFFM_CGRAM=2 their side halves run on
+        # per-column Grams, partial per rank (k_hv_cgram MODE 2 + k_fin) on the
+        # user side and replicated (the item side halves' CG in full on every
+        # rank); their cross halves take the column-tau term before the all-reduce
+        return synth.general(seed=23, m=300, n=200, fu=2, fv=2, k=8, d_user=[300, 6], d_item=[200, 5],
+                             nnz_user=1, mean_pos=5.0, test_rows=30, name="lowcard")
     # a listener-id field (D = m): every feature belongs to one rank's rows,
     # so its CG vectors stay sharded and only dot products are summed
     return synth.kkbox(seed=5, m=300, n=400, mean=12.0, name="kkbox_dist")
@@ -191,9 +199,12 @@ def _gpu_worker(rank, port, out_dir, world, name="tiny"):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["tiny", "owned"])
-def test_two_ranks_match_one_rank_on_gpu(name):
+@pytest.mark.parametrize("name,env", [("tiny", {}), ("owned", {}), ("lowcard", {"OCFFM_CGRAM": "2"}),
+                                      ("lowcard", {"OCFFM_CGRAM": "2", "OCFFM_FUSE": "0"})])
+def test_two_ranks_match_one_rank_on_gpu(name, env, monkeypatch):
     import ocffm
+    for k, v in env.items():  # inherited by the spawned ranks
+        monkeypatch.setenv(k, v)
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_gpu_worker, args=(_free_port(), d, WORLD, name), nprocs=WORLD, join=True)
         r0 = np.load(os.path.join(d, "r0.npz"))

@@ -100,15 +100,32 @@ def test_gradient_and_hv_kernels(self_side):
                 assert rel(H1, H0) <= 1e-12, ("hv", f1, f2, half)
 
 
+def test_gradient_order_independent():
+    """Gradients of side halves in any order (user side, item side, user side
+    again, then a user-side block solve): the per-segment sums the side
+    gradient passes share (k_seg_ysum, one buffer for both sides) must be
+    recomputed whenever the other side's sums replaced them."""
+    ds = synth.general(seed=5, m=60, n=40, fu=2, fv=2, k=5, nnz_user=2, mean_pos=3.0, vals="real")
+    o, g = pair(ds, with_test=False)
+    for f1, f2 in ((0, 0), (2, 2), (0, 1), (3, 3), (1, 1)):
+        for half in (0, 1):
+            assert rel(g.grad(f1, f2, half), o.grad(f1, f2, half)) <= 1e-12, (f1, f2, half)
+    o.solve_block(2, 3)
+    g.solve_block(2, 3)
+    o.solve_block(0, 0)
+    g.solve_block(0, 0)
+    assert_state(o, g, 1e-9)
+    np.testing.assert_array_equal(g.cg_log(), o.cg_log())
+
+
 KK_RC = dict(seed=3, m=1500, n=4000, mean=20.0, name="kk_rc")  # ~24 % heavy positives on both sides
 
 
-@pytest.mark.parametrize("env", [{}, {"OCFFM_NO_MFMA": "1"}, {"OCFFM_RC": "1"}, {"OCFFM_CGRAM": "2"},
+@pytest.mark.parametrize("env", [{}, {"OCFFM_NO_MFMA": "1"}, {"OCFFM_CGRAM": "2"},
                                  {"OCFFM_CGRAM": "2", "OCFFM_NO_MFMA": "1"}, {"OCFFM_TPRE": "1"}])
 def test_gradient_and_hv_fp32_k32(monkeypatch, env):
     """fp32 at k = 32 (the perf build: the cross halves' k x k Grams on MFMA,
-    kernels.hpp k_gram_mfma32; the id-field cross halves row-complete with
-    heavy-row Grams, k_hs_cross_rc, opt-in; OCFFM_CGRAM=2: every side half of a
+    kernels.hpp k_gram_mfma32; OCFFM_CGRAM=2: every side half of a
     one-node field on per-column Grams, built on MFMA by k_col_gram32 with
     multi-chunk columns summed by k_gram_slot_sum, or by k_col_gram under
     OCFFM_NO_MFMA) against the fp64 oracle: every half's gradient and
@@ -128,13 +145,9 @@ def test_gradient_and_hv_fp32_k32(monkeypatch, env):
                 assert rel(H1, H0) <= 1e-4, ("hv", f1, f2, half, rel(H1, H0))
 
 
-@pytest.mark.parametrize("env", [{}, {"OCFFM_RC": "1"}])
-def test_epochs_fp32_k32_row_complete(monkeypatch, env):
-    """Two fp32 epochs at k = 32 with the row-complete id-field cross halves
-    (OCFFM_RC=1) and without: objective of the fp32 state (evaluated in fp64) within
-    1e-3 of the oracle's; CG counts within 1 per half."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+def test_epochs_fp32_k32():
+    """Two fp32 epochs at k = 32: objective of the fp32 state (evaluated in
+    fp64) within 1e-3 of the oracle's; CG counts within 1 per half."""
     ds = synth.kkbox(**KK_RC)
     o, g = pair(ds, precision=ocffm.FP32, with_test=False)
     for _ in range(2):
@@ -275,7 +288,7 @@ def test_heavy_columns(precision, cgram, monkeypatch):
         assert abs(gpu_objective(o2, g) - f_ref) <= 1e-3 * abs(f_ref)
 
 
-@pytest.mark.parametrize("ds_name", ["heavy", "kkbox_s", "kkbox_s_fuse2", "kkbox_s_cgram2"])
+@pytest.mark.parametrize("ds_name", ["heavy", "kkbox_s", "kkbox_s_cgram2"])
 def test_fp32_runs_bit_identical(ds_name, monkeypatch):
     """The default fp32 path has no order-dependent float sums (feature
     passes, Gram builds and grid reductions combine in a fixed order): two
@@ -285,8 +298,6 @@ def test_fp32_runs_bit_identical(ds_name, monkeypatch):
         monkeypatch.setenv("OCFFM_CGRAM", "2")
         ds = synth.general(**HEAVY)
     else:
-        if ds_name.endswith("fuse2"):  # id-like row passes finalise their columns (chunk_finalize)
-            monkeypatch.setenv("OCFFM_FUSE", "2")
         if ds_name.endswith("cgram2"):  # MFMA per-column Grams (k = 32), multi-chunk slot sums
             monkeypatch.setenv("OCFFM_CGRAM", "2")
         ds = synth.kkbox(m=3000, n=4000, mean=20.0, seed=11, name="kk_det")
@@ -335,12 +346,11 @@ def test_speculative_update_bit_identical(monkeypatch):
             np.testing.assert_array_equal(a, b, err_msg=name)
 
 
-@pytest.mark.parametrize("env", [{"OCFFM_FUSE": "2"}, {"OCFFM_FUSE": "0"}, {"OCFFM_SEG_LEN": "3"}, {"OCFFM_LOOKAHEAD": "3"}, {"OCFFM_SCATTER": "1"},
-                                 {"OCFFM_FUSE": "2", "OCFFM_SEG_LEN": "2"}, {"OCFFM_CGRAM": "0"},
+@pytest.mark.parametrize("env", [{"OCFFM_FUSE": "0"}, {"OCFFM_SEG_LEN": "3"}, {"OCFFM_LOOKAHEAD": "3"},
+                                 {"OCFFM_SEG_LEN": "2"}, {"OCFFM_CGRAM": "0"},
                                  {"OCFFM_NO_FOLD": "1"}, {"OCFFM_LAZY_BASE": "0"},
                                  {"OCFFM_SPEC_FIXED": "1"}, {"OCFFM_SPEC_FIXED": "2"}, {"OCFFM_SPEC": "0"},
-                                 {"OCFFM_YSUM": "0"}, {"OCFFM_YTVIA": "0"}, {"OCFFM_FUSE": "3"},
-                                 {"OCFFM_CGSMALL": "1"}])
+                                 {"OCFFM_YSUM": "0"}, {"OCFFM_YTVIA": "0"}])
 def test_execution_variants_fp64(kk_small, monkeypatch, env):
     """Schedule knobs (id-field row fusion, segment length, CG look-ahead)
     change the kernels that run, never the result."""
@@ -380,8 +390,23 @@ def test_cli_matches_oracle_cli(tiny, tmp_path):
     a = open(tmp_path / "gpu.model").read().split("\n")
     b = open(tmp_path / "cpu.model").read().split("\n")
     assert len(a) == len(b)
-    diff = sum(x != y for x, y in zip(a, b))
-    assert diff <= len(a) // 100  # 6-significant-digit text; rounding-boundary lines only
+    # The writer itself is byte-exact on identical tables
+    # (test_boundary_gpu.py::test_text_model_byte_exact).  Here the tables are
+    # two fp64 trainings (~1e-13 apart), so a value may round to the other
+    # side of a 6th-significant-digit boundary: every token of a differing
+    # line must still be the same label or a value within one unit of the
+    # 6th significant digit.
+    ndiff = 0
+    for x, y in zip(a, b):
+        if x == y:
+            continue
+        ndiff += 1
+        tx, ty = x.split(" "), y.split(" ")
+        assert len(tx) == len(ty) and tx[0] == ty[0], (x, y)
+        for u, v in zip(tx[1:], ty[1:]):
+            fu_, fv_ = float(u), float(v)
+            assert abs(fu_ - fv_) <= 1.01e-5 * max(abs(fu_), abs(fv_)), (x, y)
+    assert ndiff <= len(a) // 100
 
 
 def test_kkbox_full_size_properties():

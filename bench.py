@@ -18,6 +18,13 @@ The JSON line also carries:
                  same K epochs right after the (uninstrumented) timed region.
   cpu_baseline — the CPU oracle (clean-room OpenMP port of the reference,
                  fp64) timed on this host on a bounded sample, rank 0, N=1.
+  modes        — (N=1) the same kkbox epochs in fp64 (the reference's own
+                 arithmetic, the parity mode); the config-5 shard (BASELINE
+                 configs[4] restated, SURVEY §8d: 2 M rows, 39+1 fields,
+                 k=64, 20 GB of P caches: past the Infinity Cache); the
+                 SGD/AdaGrad mode.  Each with its own roofline: "mfma" with
+                 TFLOP/s against the f32 MFMA peak when the dominant family's
+                 algorithmic flop/byte exceeds the ridge, else "hbm".
 """
 import argparse
 import glob
@@ -38,7 +45,10 @@ import ocffm  # noqa: E402
 import synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32), dense
+RIDGE_FLOP_PER_B = MFMA_F32_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)
 ROWS_PER_GPU = 30755
+CFG5_ROWS = 2_000_000
 
 
 def parse():
@@ -52,7 +62,92 @@ def parse():
     ap.add_argument("--cpu-single-epochs", type=int, default=1, help="one-thread oracle epochs (0: skip)")
     ap.add_argument("--sgd", choices=["auto", "off"], default="auto",
                     help="N=1: also time the SGD/AdaGrad mode (tools/bench_sgd.py) into 'modes'")
+    ap.add_argument("--modes", choices=["auto", "off"], default="auto",
+                    help="N=1: also time the fp64 parity mode and the config-5 shard into 'modes'")
+    ap.add_argument("--cfg5-steps", type=int, default=3, help="timed epochs of the config-5 mode (<= --steps)")
     return ap.parse_args()
+
+
+def run_newton(ds, prec, steps, warmup, k=32, self_side=True, world=1, rank=0, local=0, comm=None, allreduce=None,
+               pmc_tag=""):
+    """Warm-up (finds the dominant kernel family), K timed epochs (barrier +
+    device sync on both sides, max over ranks), then the same K epochs again
+    with the dominant family's dispatches carrying HIP events (roofline)."""
+    g = ocffm.problem_from_dataset(ds, precision=prec, with_test=False, device=local, rank=rank, nranks=world,
+                                   comm=comm, allreduce=allreduce, k=k, self_side=self_side)
+    ocffm.srand(1)
+    g.init()
+
+    def barrier():
+        g.sync()
+        if world > 1:
+            dist.barrier()
+
+    g.set_profiling(True)
+    for _ in range(max(1, warmup)):
+        g.one_epoch()
+    ks = g.kernel_stats()
+    dominant = max(((kk, v) for kk, v in ks.items() if not kk.startswith("half(")),
+                   key=lambda kv: kv[1]["total_ms"])[0]
+    g.reset_stats()
+    g.set_profiling(False)
+
+    # timed region: K epochs, no instrumentation (event-carrying dispatches
+    # cost ~7 us each and would perturb the wall clock)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.one_epoch()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    cg = g.cg_log()
+    alg = g.alg_bytes()
+    # kernel-timing pass: the same K epochs again, the dominant family's
+    # dispatches carrying start/stop HIP events on the solver stream
+    g.reset_stats()
+    g.set_profile_filter(dominant)
+    g.set_profiling(True)
+    for _ in range(steps):
+        g.one_epoch()
+    barrier()
+    ks = g.kernel_stats()
+    g.close()
+
+    d = ks.get(dominant, dict(launches=0, total_ms=0.0, alg_bytes=0.0, alg_flops=0.0))
+    avg_ms = d["total_ms"] / max(1, d["launches"])
+    bytes_per_launch = d["alg_bytes"] / max(1, d["launches"])
+    flops_per_launch = d.get("alg_flops", 0.0) / max(1, d["launches"])
+    if flops_per_launch > RIDGE_FLOP_PER_B * bytes_per_launch:  # an MFMA-bound family (k x k Grams / T at large C)
+        ach = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
+        roof = {"kernel": dominant, "bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_F32_PEAK_TFS,
+                "unit": "TFLOP/s", "frac": round(ach / MFMA_F32_PEAK_TFS, 4), "traffic": None,
+                "alg_flops_per_launch": flops_per_launch,
+                "achieved_GBps": round(bytes_per_launch / (avg_ms * 1e-3) / 1e9, 1) if avg_ms > 0 else 0.0}
+    else:
+        ach = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        roof = {"kernel": dominant, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
+    roof.update({"avg_launch_us": round(avg_ms * 1e3, 2), "alg_bytes_per_launch": bytes_per_launch,
+                 "launches": d["launches"], "epoch_alg_GBps": round(alg / dt / 1e9, 1),
+                 "epoch_alg_bytes": alg / max(1, steps)})
+    # HBM bytes per launch of the same kernel family from the committed
+    # rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, MI355X guide §HBM).
+    pat = f"r*_{pmc_tag}pmc_traffic.json"
+    pmcs = sorted(p for p in glob.glob(os.path.join(REPO, "profiles", pat)) if pmc_tag or "_sgd_" not in p
+                  and "_cfg5_" not in p and "_fp64_" not in p)
+    if pmcs:
+        pmc = pmcs[-1]
+        roof["traffic_source"] = os.path.relpath(pmc, REPO)
+        try:
+            t = json.load(open(pmc)).get(dominant)
+            roof["traffic"] = None if t is None else round(t["bytes_per_launch"])
+        except Exception:
+            pass
+    return dict(dt=dt, roof=roof, cg_per_epoch=round(cg.sum() / max(1, steps), 1))
 
 
 def main():
@@ -83,86 +178,27 @@ def main():
         # N = 1 on the multi-rank code path (a one-rank RCCL communicator):
         # the compute cost of that path without any real exchange
         comm = ocffm.comm_id()
-    g = ocffm.problem_from_dataset(ds, precision=prec, with_test=False, device=local, rank=rank, nranks=world,
-                                   comm=comm, allreduce=allreduce)
-    ocffm.srand(1)
-    g.init()
-
-    def barrier():
-        g.sync()
-        if world > 1:
-            dist.barrier()
-
-    # warmup; the first warmup epoch also finds the dominant kernel family
-    g.set_profiling(True)
-    for _ in range(max(1, args.warmup)):
-        g.one_epoch()
-    ks = g.kernel_stats()
-    dominant = max(((k, v) for k, v in ks.items() if not k.startswith("half(")),
-                   key=lambda kv: kv[1]["total_ms"])[0]
-    g.reset_stats()
-    g.set_profiling(False)
-
-    # timed region: K epochs, no instrumentation (event-carrying dispatches
-    # cost ~7 us each and would perturb the wall clock)
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        g.one_epoch()
-    barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    cg = g.cg_log()
-    alg = g.alg_bytes()
-    # kernel-timing pass: the same K epochs again, the dominant family's
-    # dispatches carrying start/stop HIP events on the solver stream
-    g.reset_stats()
-    g.set_profile_filter(dominant)
-    g.set_profiling(True)
-    for _ in range(args.steps):
-        g.one_epoch()
-    barrier()
-    ks = g.kernel_stats()
-
+    r = run_newton(ds, prec, args.steps, args.warmup, k=32, world=world, rank=rank, local=local, comm=comm,
+                   allreduce=allreduce, pmc_tag="" if prec == ocffm.FP32 else "fp64_")
     rows_total = ROWS_PER_GPU * world
-    value = rows_total * args.steps / dt
-    d = ks.get(dominant, dict(launches=0, total_ms=0.0, alg_bytes=0.0))
-    avg_ms = d["total_ms"] / max(1, d["launches"])
-    bytes_per_launch = d["alg_bytes"] / max(1, d["launches"])
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    roof = {"kernel": dominant, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "avg_launch_us": round(avg_ms * 1e3, 2), "alg_bytes_per_launch": bytes_per_launch,
-            "launches": d["launches"],
-            "epoch_alg_GBps": round(alg / dt / 1e9, 1),
-            "epoch_alg_bytes": alg / max(1, args.steps)}
-    # HBM bytes per launch of the same kernel family from the committed
-    # rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, MI355X guide §HBM).
-    pmcs = sorted(p for p in glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json")) if "_sgd_" not in p)
-    if pmcs:
-        pmc = pmcs[-1]
-        roof["traffic_source"] = os.path.relpath(pmc, REPO)
-        try:
-            t = json.load(open(pmc)).get(dominant)
-            roof["traffic"] = None if t is None else round(t["bytes_per_launch"])
-        except Exception:
-            pass
+    value = rows_total * args.steps / r["dt"]
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
         cpu = cpu_baseline(ds, args.cpu_epochs, args.cpu_single_epochs)
-    modes = None
-    if world == 1 and args.sgd == "auto":
-        modes = {"sgd": sgd_mode(ds, args)}
+    modes = {}
+    if world == 1 and args.modes == "auto":
+        if prec == ocffm.FP32:
+            modes["fp64"] = fp64_mode(ds, args)
+        modes["cfg5"] = cfg5_mode(args)
+        if args.sgd == "auto":
+            modes["sgd"] = sgd_mode(ds, args)
 
     if rank == 0:
         line = {
             "metric": "train instances/sec, kkbox-shape k=32; 1/2/4/8 MI355X vs CPU OpenMP",
             "value": round(value, 1), "unit": "instances/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+            "warmup": args.warmup, "ms_per_step": round(r["dt"] / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32" if prec == ocffm.FP32 else "f64",
             "data": "synthetic",
             "config": {"workload": "kkbox-shape (BASELINE configs[2]): one-class FFM block Newton-CG epoch",
@@ -170,16 +206,53 @@ def main():
                        "positives": ds.n_positives, "user_fields": 2, "item_fields": 3, "k": 32,
                        "lambda": 4.0, "omega": 0.0078125, "r": -1.0,
                        "parallelism": f"dp{world}" + ("-rccl1" if comm is not None and world == 1 else ""),
-                       "cg_iters_per_epoch": round(cg.sum() / max(1, args.steps), 1)},
-            "roofline": roof,
+                       "cg_iters_per_epoch": r["cg_per_epoch"]},
+            "roofline": r["roof"],
             "cpu_baseline": cpu,
         }
         if modes:
             line["modes"] = modes
         print(json.dumps(line), flush=True)
-    g.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def fp64_mode(ds, args):
+    """The same kkbox-shape epochs in the reference's own arithmetic (fp64,
+    ffm.h:34-35): the parity mode's speed, with its own roofline (s = 8)."""
+    try:
+        r = run_newton(ds, ocffm.FP64, args.steps, args.warmup, k=32, pmc_tag="fp64_")
+        return {"metric": "train instances/sec, kkbox-shape k=32, fp64 (parity mode)",
+                "value": round(ROWS_PER_GPU * args.steps / r["dt"], 1), "unit": "instances/s", "dtype": "f64",
+                "ms_per_step": round(r["dt"] / args.steps * 1e3, 3), "cg_iters_per_epoch": r["cg_per_epoch"],
+                "roofline": r["roof"]}
+    except Exception as e:  # never blocks the headline number
+        return {"value": None, "error": str(e)}
+
+
+def cfg5_mode(args):
+    """BASELINE configs[4] as SURVEY §8d restates it, one GPU's row shard of
+    the 100 M-row, 8-GPU run: --ns, 39 user fields of 250,000 features + the
+    item id (250,000 items), k = 64, fp32, CFG5_ROWS rows (the 39 P caches
+    alone are 20 GB: every pass streams from HBM, past the 256 MB Infinity
+    Cache).  Weak scaling at N GPUs = N such shards."""
+    try:
+        t0 = time.perf_counter()
+        ds = synth.cfg5(m=CFG5_ROWS)
+        gen = time.perf_counter() - t0
+        steps = max(1, min(args.steps, args.cfg5_steps))
+        r = run_newton(ds, ocffm.FP32, steps, 1, k=64, self_side=False, pmc_tag="cfg5_")
+        return {"metric": "train instances/sec, config-5 shard (39+1 fields, 250k feats/field, k=64, --ns)",
+                "value": round(CFG5_ROWS * steps / r["dt"], 1), "unit": "instances/s", "dtype": "f32",
+                "steps": steps, "ms_per_step": round(r["dt"] / steps * 1e3, 3),
+                "config": {"workload": "BASELINE configs[4] restated (SURVEY §8d): one GPU's row shard",
+                           "rows_per_gpu": CFG5_ROWS, "items": int(ds.item.m), "positives": ds.n_positives,
+                           "user_fields": 39, "item_fields": 1, "features_per_field": 250000, "k": 64,
+                           "self_side": False, "cg_iters_per_epoch": r["cg_per_epoch"],
+                           "p_cache_GB": round(39 * CFG5_ROWS * 64 * 4 / 1e9, 1), "datagen_s": round(gen, 1)},
+                "roofline": r["roof"]}
+    except Exception as e:  # never blocks the headline number
+        return {"value": None, "error": str(e)}
 
 
 def sgd_mode(ds, args):

@@ -208,6 +208,7 @@ typedef struct ocffm_kernel_stat {
   uint64_t launches;
   double total_ms;     /* summed event-measured duration        */
   double alg_bytes;    /* summed algorithmic bytes  */
+  double alg_flops;    /* summed floating-point ops (MFMA kernels; else 0) */
 } ocffm_kernel_stat;
 int ocffm_problem_cg_log(ocffm_problem *p, int32_t *out, int cap, int *count);
 int ocffm_problem_set_profiling(ocffm_problem *p, int on);

@@ -685,54 +685,104 @@ __global__ __launch_bounds__(BLOCK) void k_init_ytilde(uint64_t R, const int64_t
   }
 }
 
-// T_i = sum_c P_c[i] M_c for every row of a side (the w T_i term of
-// gd_cross, ffm.cpp:663-700), fp32 at KP = 32, on MFMA, before the cross
-// gradient pass (which then loads one T row per row instead of C table rows
-// and C k x k products).  In the pass, T_i cost C k^2 LDS reads per row
-// (4 KB per table: LDS-bound, ~24 KB per row at C = 6) and its registers held
-// the gathers' occupancy down: at kkbox shape the pass ran ~0.5 ms per epoch
-// faster without it.  Here one wave computes a 32-row tile as a 32 x 32 x
-// (C * 32) product: v_mfma_f32_32x32x2f32 with the rows as M and the table
-// columns as K, taken in the order (s, s + 16) so that lane l's A operands
-// are 16 consecutive floats of its row (row l % 32, floats 16 (l / 32) ..
-// + 15: four 16-B loads per table, all issued before the first MFMA); B =
-// M_c (staged once per block in LDS), lane l reads M_c[s + 16 (l / 32)][l % 32].
-template <int L>
-__global__ __launch_bounds__(BLOCK) void k_rows_T32(uint64_t R, const float *const *__restrict__ P,
-                                                    const float *__restrict__ M, float *__restrict__ T) {
+// T_i = sum_c A_c[i] M_c for every row of a side (the w T_i term of
+// gd_cross, ffm.cpp:663-700, T = sum_a P_a (Q_a^T Q1)), fp32 at KP = 32 or
+// 64, on MFMA, ahead of the cross gradient pass (which then loads one T row
+// per row instead of C table rows and C k x k products).  In the pass, T_i
+// costs C k^2 multiply-adds per row with M read from LDS (or, when the C
+// Grams exceed 64 KB, from L2: at BASELINE config 5, C = 39 and k = 64, that
+// is 624 KB of M per row).  Here T = [A_1 .. A_C] [M_1; ..; M_C] is a
+// (R x C KP) by (C KP x KP) product on v_mfma_f32_32x32x2f32: each wave owns
+// TW tiles of 32 rows x KP columns (KP/32 accumulators of 16 registers per
+// tile); the K dimension (table c, column k) is taken in the order (s, s +
+// KP/2) so that lane l's A operands are the KP/2 consecutive floats
+// [KP/2 (l/32), +KP/2) of row l%32 (KP/8 16-B loads per table and tile, the
+// next table's in flight during this table's MFMAs).  B = M_c from LDS,
+// staged TG tables at a time (one block per CU, 8 waves: 512 rows share
+// each staging); Ms[(c k 32 + e) NT + t] = M_c[k][32 t + e], so one
+// ds_read_b64 (KP = 64) gives a lane both output tiles' operands.
+constexpr int TBLOCK = 512;  // threads of a k_rows_T block
+template <int KP> struct RowsT {
+  static constexpr int NT = KP / 32;  // 32-column output tiles
+  static constexpr int KH = KP / 2;   // K steps per table (two K values each)
+  static constexpr int TW = 2;        // 32-row tiles per wave
+  static constexpr int TG = KP == 64 ? 8 : 32;  // tables per LDS stage (128 KB)
+  static constexpr int ROWS = (TBLOCK / 64) * TW * 32;  // rows per block pass
+};
+template <int KP>
+__global__ __launch_bounds__(TBLOCK) void k_rows_T(uint64_t R, int C, const float *const *__restrict__ A,
+                                                   const float *__restrict__ M, float *__restrict__ T) {
+  using RT = RowsT<KP>;
+  constexpr int NT = RT::NT, KH = RT::KH, TW = RT::TW, TG = RT::TG;
   typedef float f16x __attribute__((ext_vector_type(16)));
-  __shared__ float Ms[L * 1024];
-  for (int t = threadIdx.x; t < L * 1024; t += BLOCK) Ms[t] = M[t];
-  __syncthreads();
-  const int lane = threadIdx.x & 63, e = lane & 31, hf = lane >> 5;
-  BufView pb[L];
+  typedef float v2f __attribute__((ext_vector_type(2)));
+  __shared__ __align__(16) float Ms[TG * KP * KP];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int e = lane & 31, hf = lane >> 5;
+  const uint32_t rowb = KP * 4;
+  for (uint64_t base = (uint64_t)blockIdx.x * RT::ROWS; base < R; base += (uint64_t)gridDim.x * RT::ROWS) {
+    f16x acc[TW][NT];
 #pragma unroll
-  for (int c = 0; c < L; c++) pb[c] = buf_view(P[c], R * 128);
-  const uint64_t ntiles = (R + 31) / 32;
-  const uint64_t wave = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
-  const uint64_t nw = ((uint64_t)gridDim.x * BLOCK) >> 6;
-  for (uint64_t tile = wave; tile < ntiles; tile += nw) {
-    const uint64_t row = tile * 32 + e;  // rows past R read zero (buffer range)
-    f4v a[L][4];
+    for (int t = 0; t < TW; t++)
 #pragma unroll
-    for (int c = 0; c < L; c++)
+      for (int n = 0; n < NT; n++)
 #pragma unroll
-      for (int q = 0; q < 4; q++) a[c][q] = bld<float>(pb[c], (uint32_t)(row * 128 + hf * 64 + q * 16));
-    f16x acc;
+        for (int r = 0; r < 16; r++) acc[t][n][r] = 0.0f;
+    // rows of this wave's tiles: row (base + (w TW + t) 32 + e); past R: zero (buffer range)
+    for (int g0 = 0; g0 < C; g0 += TG) {
+      const int ng = C - g0 < TG ? C - g0 : TG;
+      __syncthreads();  // the previous stage's readers are done
+      for (int q = threadIdx.x; q < ng * KP * KP; q += TBLOCK) {
+        const int c = q / (KP * KP), rem = q % (KP * KP), k = rem / KP, col = rem % KP;
+        Ms[((c * KP + k) * 32 + (col & 31)) * NT + (col >> 5)] = M[(size_t)(g0 + c) * KP * KP + rem];
+      }
+      __syncthreads();
+      f4v a[2][TW][KH / 4];
+      auto load = [&](int sb, int c) {
+        const BufView ab = buf_view(A[g0 + c], R * rowb);
 #pragma unroll
-    for (int r = 0; r < 16; r++) acc[r] = 0.0f;
+        for (int t = 0; t < TW; t++) {
+          const uint64_t row = base + (uint64_t)(w * TW + t) * 32 + e;
+          const uint32_t off = row < R ? (uint32_t)(row * rowb + hf * KH * 4) : ab.oob;
 #pragma unroll
-    for (int c = 0; c < L; c++)
+          for (int q = 0; q < KH / 4; q++) a[sb][t][q] = bld<float>(ab, off + q * 16);
+        }
+      };
+      load(0, 0);
+      for (int c = 0; c < ng; c++) {
+        const int sb = c & 1;
+        if (c + 1 < ng) load(sb ^ 1, c + 1);
+        const float *mc = Ms + (size_t)c * KP * KP;
 #pragma unroll
-      for (int s = 0; s < 16; s++)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c][s >> 2][s & 3], Ms[c * 1024 + (s + 16 * hf) * 32 + e], acc, 0,
-                                                   0, 0);
-    // D register r of lane l: row m = 8(r/4) + 4(l/32) + r%4 of the tile, column l%32
+        for (int s = 0; s < KH; s++) {
+          const int k = s + KH * hf;
+          if constexpr (NT == 2) {
+            const v2f b = *reinterpret_cast<const v2f *>(mc + (k * 32 + e) * 2);
 #pragma unroll
-    for (int r = 0; r < 16; r++) {
-      const uint64_t m = tile * 32 + 8 * (r >> 2) + 4 * hf + (r & 3);
-      if (m < R) T[m * 32 + e] = acc[r];
+            for (int t = 0; t < TW; t++) {
+              const float av = a[sb][t][s >> 2][s & 3];
+              acc[t][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b[0], acc[t][0], 0, 0, 0);
+              acc[t][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b[1], acc[t][1], 0, 0, 0);
+            }
+          } else {
+            const float b = mc[k * 32 + e];
+#pragma unroll
+            for (int t = 0; t < TW; t++)
+              acc[t][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[sb][t][s >> 2][s & 3], b, acc[t][0], 0, 0, 0);
+          }
+        }
+      }
     }
+    // D register r of lane l: row 8(r/4) + 4(l/32) + r%4 of the tile, column l%32 (+32 n)
+#pragma unroll
+    for (int t = 0; t < TW; t++)
+#pragma unroll
+      for (int n = 0; n < NT; n++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          const uint64_t m = base + (uint64_t)(w * TW + t) * 32 + 8 * (r >> 2) + 4 * hf + (r & 3);
+          if (m < R) T[m * KP + n * 32 + e] = acc[t][n][r];
+        }
   }
 }
 
@@ -765,7 +815,7 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
                                                         const real *__restrict__ ytv) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP, OCFFM_GD_GB>;
-  // TP: T_i precomputed by k_rows_T32 (one row load; no M in LDS)
+  // TP: T_i precomputed by k_rows_T (one row load; no M in LDS)
   // ytv (BM_IN): the stored value is read from the other orientation through
   // perm (ytv[perm[q]]), so the entering pass of the block needs no refresh
   // of this orientation (solver.hip gradient)
@@ -1910,6 +1960,122 @@ __global__ __launch_bounds__(BLOCK) void k_gram_mfma32(uint64_t Rp, const float 
     out[(size_t)L * 1024 + 32 + threadIdx.x] = redc[1][threadIdx.x];
   }
   if (threadIdx.x == 0) out[(size_t)L * 1024 + 64] = redc[2][0];
+}
+
+// Cross-half aggregates at KP = 64, fp32, on MFMA (gd_cross / cg,
+// ffm.cpp:660-670, 767-771): M_c = A_c^T B for every partner-side table A_c
+// (k x k, c < C), oQ = sum_i B_i, bQ = sum_i wv_i B_i and sum wv, over the
+// rows of block x's chunk.  Each wave owns GW tables (4 x 16 accumulator
+// registers per table: the 2 x 2 tiles of 32 x 32) and walks every row of
+// the chunk: v_mfma_f32_32x32x2f32 takes a row pair as the K dimension,
+// lane l supplying A_c[row 2u + l/32][32 mt + l%32] and B[row][32 nt + l%32]
+// (dword loads: a half-wave reads one 128-B half-row), two register sets so
+// that the next round's loads are in flight.  The block's four waves read
+// the same B rows (L1 hits) for four table groups.  Block b takes table
+// group b % ng and row chunk b / ng, so the blocks of one chunk are
+// dispatched together and share its B rows in the Infinity Cache.
+// Partials: part[chunk][c * 4096 + m * 64 + n] and, from group 0, wave 0,
+// the sums at [C * 4096 ..) (k_reduce_parts, fixed order).
+constexpr int GW64 = 1;  // tables per wave of k_gram_mfma64 (64 accumulators each)
+static __global__ __launch_bounds__(BLOCK) void k_gram_mfma64(uint64_t Rp, int C, const float *const *__restrict__ A,
+                                                       const float *__restrict__ B, const float *__restrict__ wv,
+                                                       float *__restrict__ part, uint64_t nout,
+                                                       uint64_t rows_per_block, unsigned ngroups) {
+  typedef float f16x __attribute__((ext_vector_type(16)));
+  constexpr int U = 4;  // row pairs per round
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int e = lane & 31, hf = lane >> 5;
+  const unsigned grp = blockIdx.x % ngroups, chunk = blockIdx.x / ngroups;
+  const int c0 = (int)(grp * (BLOCK / 64) + w) * GW64;
+  const int nc = C - c0 < 0 ? 0 : (C - c0 < GW64 ? C - c0 : GW64);  // wave-uniform
+  const bool sums = grp == 0 && w == 0;
+  if (nc == 0) return;  // no barrier below
+  f16x acc[GW64][4];
+#pragma unroll
+  for (int c = 0; c < GW64; c++)
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) acc[c][t][r] = 0.0f;
+  BufView ab[GW64];
+#pragma unroll
+  for (int c = 0; c < GW64; c++) ab[c] = buf_view(c < nc ? A[c0 + c] : nullptr, c < nc ? Rp * 256 : 0);
+  const BufView bb = buf_view(B, Rp * 256), wb = buf_view(wv, wv ? Rp * 4 : 0);
+  const uint64_t r0 = (uint64_t)chunk * rows_per_block;
+  const uint64_t r1 = r0 + rows_per_block < Rp ? r0 + rows_per_block : Rp;
+  float cs[2] = {0, 0}, ws[2] = {0, 0}, wt = 0;
+  float bv[2][U][2], av[2][U][GW64][2], wvv[2][U];
+  auto load = [&](int sb, uint64_t j0) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t jj = j0 + 2 * u + hf;
+      const bool ok = jj < r1;
+      const uint32_t off = ok ? (uint32_t)(jj * 256 + e * 4) : 0xffffff00u;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        bv[sb][u][h] = bld1<float>(bb, off + h * 128);
+#pragma unroll
+        for (int c = 0; c < GW64; c++) av[sb][u][c][h] = bld1<float>(ab[c], off + h * 128);
+      }
+      wvv[sb][u] = bld1<float>(wb, ok ? (uint32_t)(jj * 4) : 0xffffff00u);
+    }
+  };
+  auto step = [&](int sb) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+#pragma unroll
+      for (int c = 0; c < GW64; c++)
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+          for (int nt = 0; nt < 2; nt++)
+            acc[c][mt * 2 + nt] =
+                __builtin_amdgcn_mfma_f32_32x32x2f32(av[sb][u][c][mt], bv[sb][u][nt], acc[c][mt * 2 + nt], 0, 0, 0);
+      if (sums) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          cs[h] += bv[sb][u][h];
+          ws[h] += wvv[sb][u] * bv[sb][u][h];
+        }
+        if (e == 0) wt += wvv[sb][u];
+      }
+    }
+  };
+  // rows past r1 load zeros (buffer range check), so a trailing round is harmless
+  for (uint64_t j0 = r0; j0 < r1; j0 += 4 * U) {
+    load(0, j0);
+    load(1, j0 + 2 * U);
+    step(0);
+    step(1);
+  }
+  float *out = part + (size_t)chunk * nout;
+#pragma unroll
+  for (int c = 0; c < GW64; c++) {
+    if (c >= nc) break;
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int m = (t >> 1) * 32 + 8 * (r >> 2) + 4 * hf + (r & 3), n = (t & 1) * 32 + e;
+        out[(size_t)(c0 + c) * 4096 + m * 64 + n] = acc[c][t][r];
+      }
+  }
+  if (sums) {  // the two half-waves hold the even / odd rows of the same column
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      cs[h] += __shfl_xor(cs[h], 32, 64);
+      ws[h] += __shfl_xor(ws[h], 32, 64);
+    }
+    wt += __shfl_xor(wt, 32, 64);
+    if (hf == 0) {
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        out[(size_t)C * 4096 + h * 32 + e] = cs[h];
+        out[(size_t)C * 4096 + 64 + h * 32 + e] = ws[h];
+      }
+      if (e == 0) out[(size_t)C * 4096 + 128] = wt;
+    }
+  }
 }
 
 // o in [0, cnt): t = sum_b part[b][off + o]; o < split -> out_real[o] = t,

@@ -77,7 +77,7 @@ static unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap = 4096
 // -------------------------------------------------------------- profiling
 struct KStat {
   uint64_t launches = 0;
-  double ms = 0, bytes = 0;
+  double ms = 0, bytes = 0, flops = 0;
 };
 
 // ------------------------------------------------------------------- data
@@ -1158,7 +1158,9 @@ template <typename real> class Problem final : public ProblemBase {
     hipExtLaunchKernelGGL(k, grid, block, (uint32_t)smem, stream_, e0, arm_b_, 0u, static_cast<KArgs>(a)...);
     HIPCHK(hipGetLastError());
   }
-  template <class L> void prof_launch(const char *name, double bytes, L &&body) {
+  // bytes / flops: the launch's algorithmic HBM bytes and (MFMA kernels)
+  // floating-point operations, for the roofline of its family
+  template <class L> void prof_launch(const char *name, double bytes, L &&body, double flops = 0) {
     if (!profiling || (!prof_filter.empty() && prof_filter != name)) {
       body();
       HIPCHK(hipGetLastError());
@@ -1173,7 +1175,7 @@ template <typename real> class Problem final : public ProblemBase {
       HIPCHK(hipEventRecord(arm_a_, stream_));
       HIPCHK(hipEventRecord(arm_b_, stream_));
     }
-    pending_.push_back({name, bytes, arm_a_, arm_b_, prof_tag_});
+    pending_.push_back({name, bytes, arm_a_, arm_b_, prof_tag_, flops});
     arm_a_ = arm_b_ = nullptr;
     arm_first_ = false;
   }
@@ -1198,6 +1200,7 @@ template <typename real> class Problem final : public ProblemBase {
       k.launches++;
       k.ms += ms;
       k.bytes += p.bytes;
+      k.flops += p.flops;
       ev_free_.push_back(p.a);
       ev_free_.push_back(p.b);
     }
@@ -1267,6 +1270,10 @@ template <typename real> class Problem final : public ProblemBase {
 
   void aggregates(uint64_t Rp, int L, const real *const *A, const real *B, const real *wv, real *M) {
     const size_t rs = sizeof(real);
+    if (mfma_gram64(L, Rp)) {  // fp32, KP = 64: every table in one launch (k_gram_mfma64)
+      gram64(Rp, L, A, B, wv, M);
+      return;
+    }
     const int TR = kp_ >= 64 ? 16 : 32;
     // tables per launch so the LDS stage fits in 64 KB (MFMA path: its register budget)
     const bool mg = mfma_gram(L) && (uint64_t)Rp * 128 < 0xffffff00ull;  // buffer-load offsets are 32-bit
@@ -1281,6 +1288,34 @@ template <typename real> class Problem final : public ProblemBase {
       l0 += Lc;
       first = false;
     } while (l0 < L);
+  }
+
+  // KP = 64 fp32 Grams on MFMA: gy groups of 4 GW64 tables x nbx row
+  // chunks; one launch over all L tables, f32 partials per row chunk summed
+  // in chunk order (k_reduce_parts).  ~1,024 blocks of 4 waves.
+  bool mfma_gram64(int L, uint64_t Rp) const {
+    return std::is_same<real, float>::value && kp_ == 64 && L >= 1 && !no_mfma_ && B_ok(Rp);
+  }
+  static bool B_ok(uint64_t Rp) { return Rp * 256 < 0xffffff00ull; }  // 32-bit buffer offsets
+  void gram64(uint64_t Rp, int L, const real *const *A, const real *B, const real *wv, real *M) {
+    if (!M || !B) throw Error(OCFFM_E_STATE, "gram64: Grams and partner table required");
+    constexpr int TPB = (BLOCK / 64) * GW64;  // tables per block
+    const unsigned gy = (unsigned)((L + TPB - 1) / TPB);
+    const uint64_t nout = (uint64_t)L * 4096 + 129;
+    uint64_t nbx = std::max<uint64_t>(1, std::min<uint64_t>((Rp + 63) / 64, std::max<uint64_t>(1, gram64_blocks_ / gy)));
+    const uint64_t rpb = ((Rp + nbx - 1) / nbx + 15) / 16 * 16;  // whole rounds of row pairs
+    nbx = std::max<uint64_t>(1, (Rp + rpb - 1) / rpb);
+    if (gpart64_.n < nbx * nout) gpart64_.alloc(nbx * nout, false);
+    const double abytes = (double)Rp * ((L + (B ? 1 : 0)) * 64 + (wv ? 1 : 0)) * sizeof(real);
+    prof_launch("aggregates", abytes, [&] {
+      launch(k_gram_mfma64, (unsigned)(nbx * gy), BLOCK, 0, Rp, L, (const float *const *)A, (const float *)B,
+             (const float *)wv, gpart64_.p, nout, rpb, gy);
+    }, 2.0 * Rp * L * 64 * 64);
+    const uint64_t ng = (uint64_t)L * 4096, cnt = ng + 129;
+    prof_launch("aggr_reduce", (double)nbx * cnt * 4, [&] {
+      launch(k_reduce_parts<real, float>, (unsigned)((cnt + 15) / 16), BLOCK, 0, nbx, nout, (uint64_t)0, cnt,
+             (const float *)gpart64_.p, ng, M, sums_.p);
+    });
   }
 
   void launch_aggr(uint64_t Rp, int L, const real *const *A, const real *B, const real *wv, real *M, bool sums,
@@ -1488,27 +1523,16 @@ template <typename real> class Problem final : public ProblemBase {
         // inside the block (BM_IN): read the stored value through perm from
         // the orientation the entering pass wrote (no refresh in between)
         const bool via = ytvia_ && cur && !enter;
-        // T_i = sum_c P_c[i] M_c on MFMA ahead of the pass (k_rows_T32)
+        // T_i = sum_c P_c[i] M_c on MFMA ahead of the pass (k_rows_T), where
+        // the C Grams do not fit the pass's LDS (or OCFFM_TPRE=1)
         const bool tp = tpre(own.R);
         if (tp) {
-          if constexpr (std::is_same<real, float>::value && KP == 32) {
+          if constexpr (std::is_same<real, float>::value && (KP == 32 || KP == 64)) {
+            const uint64_t nb = (own.R + RowsT<KP>::ROWS - 1) / RowsT<KP>::ROWS;
             prof_launch("rows_T", (double)C_ * own.R * KP * rs + (double)own.R * KP * rs + (double)C_ * KP * KP * rs, [&] {
-              auto gt = [&](auto lc) {
-                constexpr int LC = decltype(lc)::value;
-                launch(k_rows_T32<LC>, grid_for((own.R + 31) / 32, 4, tpre_blocks_), BLOCK, 0, (uint64_t)own.R,
-                       (const float *const *)(tabs_.p + (h.user ? 0 : C_)), (const float *)M_.p, (float *)Tpre_.p);
-              };
-              switch (C_) {  // the table count is a compile-time constant of the kernel
-                case 1: gt(std::integral_constant<int, 1>()); break;
-                case 2: gt(std::integral_constant<int, 2>()); break;
-                case 3: gt(std::integral_constant<int, 3>()); break;
-                case 4: gt(std::integral_constant<int, 4>()); break;
-                case 5: gt(std::integral_constant<int, 5>()); break;
-                case 6: gt(std::integral_constant<int, 6>()); break;
-                case 7: gt(std::integral_constant<int, 7>()); break;
-                default: gt(std::integral_constant<int, 8>()); break;
-              }
-            });
+              launch(k_rows_T<KP>, (unsigned)std::min<uint64_t>(nb, tpre_blocks_), TBLOCK, 0, (uint64_t)own.R, (int)C_,
+                     (const float *const *)(tabs_.p + (h.user ? 0 : C_)), (const float *)M_.p, (float *)Tpre_.p);
+            }, 2.0 * own.R * C_ * KP * KP);
           }
         }
         auto go2 = [&](auto ml, auto bm) {
@@ -1523,7 +1547,7 @@ template <typename real> class Problem final : public ProblemBase {
                 TP ? (const real *)Tpre_.p : (const real *)nullptr,
                 via ? (const real *)h.partner->yt.p : (const real *)nullptr);
           };
-          if constexpr (std::is_same<real, float>::value && KP == 32 && ML) {
+          if constexpr (std::is_same<real, float>::value && (KP == 32 || KP == 64) && !ML) {
             if (tp) {
               go3(std::true_type());
               return;
@@ -1536,8 +1560,9 @@ template <typename real> class Problem final : public ProblemBase {
           else if (enter) go2(ml, std::integral_constant<int, BM_ENTER>());
           else go2(ml, std::integral_constant<int, BM_IN>());
         };
+        if (tp) bytes += (double)own.R * KP * rs - (double)C_ * own.R * KP * rs;  // one T row instead of C table rows
         prof_launch("gd_cross_row", bytes, [&] {
-          if (lds) go(std::true_type());
+          if (lds && !tp) go(std::true_type());
           else go(std::false_type());
         });
         // the other orientation: refreshed here, or read through perm by the
@@ -1998,7 +2023,7 @@ template <typename real> class Problem final : public ProblemBase {
       HIPCHK(hipEventRecord(he, stream_));
       char name[32];
       std::snprintf(name, sizeof(name), "half(%u,%u)%c", f1, f2, which ? 'H' : 'W');
-      pending_.push_back({name, 0.0, hb, he, 0});
+      pending_.push_back({name, 0.0, hb, he, 0, 0.0});
     }
   }
 
@@ -2115,17 +2140,21 @@ template <typename real> class Problem final : public ProblemBase {
   // from the user orientation (k_gd_cross_seg ytv) instead of a refresh after
   // each entering pass.  OCFFM_YTVIA=0: refresh.
   bool ytvia_ = !std::getenv("OCFFM_YTVIA") || std::atoi(std::getenv("OCFFM_YTVIA")) != 0;
-  // T_i of the cross gradient passes precomputed on MFMA (k_rows_T32; fp32,
-  // KP = 32, at most 8 cross tables).  Opt-in (OCFFM_TPRE=1): measured a wash
-  // at kkbox shape (the pass gets 25 / 13 us faster per item / user
-  // half, the pre-pass costs 26.8 / 10.8 us: it must read the C tables' rows,
-  // 77 MB on the item half, which the pass had overlapped with its gathers).
+  // T_i of the cross gradient passes precomputed on MFMA (k_rows_T; fp32,
+  // KP = 32 or 64).  On where the C cross Grams exceed the pass's 64 KB of
+  // LDS (BASELINE config 5: 39 Grams of 64 x 64, 624 KB: the pass would read
+  // them from L2 for every row); elsewhere opt-in (OCFFM_TPRE=1): measured a
+  // wash at kkbox shape (the pass gets 25 / 13 us faster per item /
+  // user half, the pre-pass costs 26.8 / 10.8 us: it must read the C tables'
+  // rows, 77 MB on the item half, which the pass had overlapped with its gathers).
   bool tpre_on_ = std::getenv("OCFFM_TPRE") && std::atoi(std::getenv("OCFFM_TPRE")) != 0;
   DevBuf<real> Tpre_;
-  unsigned tpre_blocks_ = std::getenv("OCFFM_TPRE_BLOCKS") ? (unsigned)std::max(1, std::atoi(std::getenv("OCFFM_TPRE_BLOCKS"))) : 512;
+  // grid cap: one 512-thread block per CU (128 KB of LDS each)
+  unsigned tpre_blocks_ = std::getenv("OCFFM_TPRE_BLOCKS") ? (unsigned)std::max(1, std::atoi(std::getenv("OCFFM_TPRE_BLOCKS"))) : 256;
   bool tpre(uint64_t R) const {
-    return tpre_on_ && std::is_same<real, float>::value && kp_ == 32 && C_ >= 1 && C_ <= 8 && R > 0 &&
-           (uint64_t)R * 128 < 0xffffff00ull && (size_t)C_ * kp_ * kp_ * sizeof(real) <= 64 * 1024;
+    const bool big = (size_t)C_ * kp_ * kp_ * sizeof(real) > 64 * 1024;
+    return (tpre_on_ || big) && std::is_same<real, float>::value && (kp_ == 32 || kp_ == 64) && C_ >= 1 && R > 0 &&
+           (uint64_t)R * kp_ * sizeof(real) < 0xffffff00ull && !no_mfma_;
   }
   DevBuf<real> ysum_;
   void ysum_dirty() { ysum_ok_[0] = ysum_ok_[1] = false; }
@@ -2145,6 +2174,8 @@ template <typename real> class Problem final : public ProblemBase {
   // (cgram_rows: 256 rows at k = 32 fp32)
   uint64_t cgram_chunk_ = std::getenv("OCFFM_CGRAM_CHUNK") ? std::max(1, std::atoi(std::getenv("OCFFM_CGRAM_CHUNK"))) : 128;
   bool no_mfma_ = std::getenv("OCFFM_NO_MFMA") != nullptr;  // Grams on the VALU kernel instead
+  DevBuf<float> gpart64_;  // k_gram_mfma64 partials
+  uint64_t gram64_blocks_ = std::getenv("OCFFM_GRAM64_BLOCKS") ? std::strtoull(std::getenv("OCFFM_GRAM64_BLOCKS"), nullptr, 10) : 1024;
   uint64_t gram_blocks_ = std::getenv("OCFFM_GRAM_BLOCKS") ? std::strtoull(std::getenv("OCFFM_GRAM_BLOCKS"), nullptr, 10) : 512;
   bool no_owned_ = false;
   bool owned_stale_ = false;  // owned tables differ across ranks until sync_owned()
@@ -2186,6 +2217,7 @@ template <typename real> class Problem final : public ProblemBase {
     double bytes;
     hipEvent_t a, b;
     int tag;  // CG iteration of a Hessian-vector launch, -1 a speculative update, 0 other
+    double flops;
   };
   int prof_tag_ = 0;
   std::vector<Pending> pending_;
@@ -2483,6 +2515,7 @@ int ocffm_problem_kernel_stats(ocffm_problem *prob, ocffm_kernel_stat *out, int 
         out[i].launches = kv.second.launches;
         out[i].total_ms = kv.second.ms;
         out[i].alg_bytes = kv.second.bytes;
+        out[i].alg_flops = kv.second.flops;
       }
       i++;
     }

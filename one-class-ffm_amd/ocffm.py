@@ -51,7 +51,7 @@ class _Metrics(C.Structure):
 
 class _KStat(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", C.c_uint64), ("total_ms", C.c_double),
-                ("alg_bytes", C.c_double)]
+                ("alg_bytes", C.c_double), ("alg_flops", C.c_double)]
 
 
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p)
@@ -471,7 +471,8 @@ class ImpProblem:
         arr = (_KStat * max(1, n.value))()
         _check(lib().ocffm_problem_kernel_stats(self.h, arr, n.value, C.byref(n)))
         return {arr[i].name.decode(): dict(launches=arr[i].launches, total_ms=arr[i].total_ms,
-                                           alg_bytes=arr[i].alg_bytes) for i in range(n.value)}
+                                           alg_bytes=arr[i].alg_bytes, alg_flops=arr[i].alg_flops)
+                for i in range(n.value)}
 
     def reset_stats(self) -> None:
         _check(lib().ocffm_problem_reset_stats(self.h))

@@ -246,6 +246,65 @@ def test_variants_fp64(variant):
     np.testing.assert_allclose(vg["ndcg"], vo["ndcg"], atol=1e-12)
 
 
+# BASELINE configs[4] (SURVEY §8d restated): --ns, 39 user fields + 1 item
+# field, k = 64.  39 cross blocks: the C = 39 Grams of 64 x 64 (624 KB) do not
+# fit the gradient pass's LDS.
+def _cfg5_small(m=300, n=60, k=64, fu=39, seed=41, test_rows=30):
+    return synth.general(seed=seed, m=m, n=n, fu=fu, fv=1, k=k, d_user=[max(4, m // 6)] * fu, d_item=[n],
+                         mean_pos=4.0, test_rows=test_rows, name="cfg5_small")
+
+
+def test_cfg5_shape_fp64():
+    """Config-5 structure at test size in the parity mode: one epoch of all
+    78 halves against the oracle within 1e-9, identical CG counts, and the
+    validation metrics (ffm.cpp:852-870, 630-703 with C = 39)."""
+    ds = _cfg5_small()
+    o, g = pair(ds, self_side=False, k=64)
+    o.one_epoch()
+    g.one_epoch()
+    assert_state(o, g, 1e-9)
+    np.testing.assert_array_equal(g.cg_log(), o.cg_log())
+    vo, vg = o.validate(), g.validate()
+    assert abs(vg["loss"] - vo["loss"]) <= 1e-9 * abs(vo["loss"])
+    np.testing.assert_allclose(vg["ndcg"], vo["ndcg"], atol=1e-12)
+
+
+@pytest.mark.parametrize("k,fu", [(64, 39), (32, 20)])
+def test_cfg5_shape_fp32_mfma(k, fu):
+    """The fp32 perf path at config-5 structure: the cross halves' T_i on MFMA
+    ahead of the gradient pass (k_rows_T<KP>: the C Grams exceed 64 KB of
+    LDS) and, at k = 64, the C cross Grams on MFMA (k_gram_mfma64), checked
+    per half against the fp64 oracle (gradient and Hessian-vector within
+    1e-4 of their largest entry) on 2,000 rows (several row chunks per
+    block of both kernels, ragged tails)."""
+    ds = _cfg5_small(m=2003, n=301, k=k, fu=fu, seed=43, test_rows=0)
+    o, g = pair(ds, precision=ocffm.FP32, self_side=False, k=k, with_test=False)
+    rng = np.random.default_rng(5)
+    for f1 in (0, fu // 2, fu - 1):
+        for half in (0, 1):
+            G0, G1 = o.grad(f1, fu, half), g.grad(f1, fu, half)
+            assert rel(G1, G0) <= 1e-4, ("grad", f1, half, rel(G1, G0))
+            v = rng.standard_normal(G0.size)
+            H0, H1 = o.hv(f1, fu, half, v), g.hv(f1, fu, half, v)
+            assert rel(H1, H0) <= 1e-4, ("hv", f1, half, rel(H1, H0))
+
+
+def test_cfg5_shape_fp32_epochs():
+    """Two fp32 epochs at config-5 structure (k = 64): objective of the fp32
+    state (evaluated in fp64 by the oracle) within 1e-3 of the oracle's."""
+    ds = _cfg5_small(m=800, n=120, seed=47, test_rows=0)
+    o, g = pair(ds, precision=ocffm.FP32, self_side=False, k=64, with_test=False)
+    for _ in range(2):
+        o.one_epoch()
+        g.one_epoch()
+    f_ref = o.func()
+    o2 = O.Oracle(ds, self_side=False, k=64, with_test=False)
+    ocffm.srand(1)
+    o2.init()
+    assert abs(gpu_objective(o2, g) - f_ref) <= 1e-3 * abs(f_ref)
+    assert np.abs(g.cg_log().astype(int) - o.cg_log().astype(int)).max() <= 1
+
+
 def test_kkbox_small_fp64(kk_small):
     o, g = pair(kk_small)
     o.one_epoch()

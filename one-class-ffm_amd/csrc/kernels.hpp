@@ -1420,7 +1420,7 @@ template <typename real, int KP, int MODE, int JE = JOB_ENT, bool TAU = false>
 __global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__restrict__ jobs,
                                                 const uint32_t *__restrict__ crow, const real *__restrict__ cval,
                                                 const real *__restrict__ h, uint64_t hbytes, real *__restrict__ wpart,
-                                                Fin<real> f, const real *__restrict__ QTQ) {
+                                                uint64_t wbytes, Fin<real> f, const real *__restrict__ QTQ) {
   using G = Geo<real, KP>;
   if (f.it > 0 && !f.st->run[f.it]) return;
   // TAU (MODE 1, and MODE 2 on several ranks): QTQ staged in LDS for the
@@ -1447,26 +1447,32 @@ __global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__res
     FinOps<real> ops;
     if (MODE != 2) ops = fin_load<real, KP, (MODE == 2 ? 0 : MODE)>(f, jb.col == JOB_NONE ? 0u : jb.col, upd, li);
     constexpr int U = (JE + G::LPR - 1) / G::LPR;
-    uint32_t rr[U];
-    real vv[U];
+    // a light job is one round of <= JE entries; a wave-chunk of a heavy
+    // column gives each subgroup several rounds (build_csc sizes them)
+    vec_t<real> s = vzero<real>();
+    int64_t b0 = jb.b;
+    do {
+      uint32_t rr[U];
+      real vv[U];
 #pragma unroll
-    for (int t = 0; t < U; t++) {
-      const int e = li + t * G::LPR;
-      const bool ok = e < JE && jb.b + e < jb.e;
-      rr[t] = ok ? crow[jb.b + e] : 0u;
-      vv[t] = ok ? cval[jb.b + e] : (real)0;
-    }
-    vec_t<real> hv[JE];
-    sfor<JE>([&](auto E) {
-      constexpr int e = decltype(E)::value;
-      const uint32_t r = sg_bcast<G::LPR, e % G::LPR>(rr[e / G::LPR], li);
-      const real x = sg_bcast<G::LPR, e % G::LPR>(vv[e / G::LPR], li);
-      const uint32_t off = jb.b + e < jb.e ? r * (uint32_t)(KP * sizeof(real)) + li * 16u : hb.oob;
-      hv[e] = vsplat<real>(x) * bld<real>(hb, off);
-    });
-    vec_t<real> s = hv[0];
+      for (int t = 0; t < U; t++) {
+        const int e = li + t * G::LPR;
+        const bool ok = e < JE && b0 + e < jb.e;
+        rr[t] = ok ? crow[b0 + e] : 0u;
+        vv[t] = ok ? cval[b0 + e] : (real)0;
+      }
+      vec_t<real> hv[JE];
+      sfor<JE>([&](auto E) {
+        constexpr int e = decltype(E)::value;
+        const uint32_t r = sg_bcast<G::LPR, e % G::LPR>(rr[e / G::LPR], li);
+        const real x = sg_bcast<G::LPR, e % G::LPR>(vv[e / G::LPR], li);
+        const uint32_t off = b0 + e < jb.e ? r * (uint32_t)(KP * sizeof(real)) + li * 16u : hb.oob;
+        hv[e] = vsplat<real>(x) * bld<real>(hb, off);
+      });
 #pragma unroll
-    for (int e = 1; e < JE; e++) s += hv[e];
+      for (int e = 0; e < JE; e++) s += hv[e];
+      b0 += JE;
+    } while (b0 < jb.e);
     bool mine = jb.col != JOB_NONE;
     if (jb.flags & 1u) {  // wave job (wave-uniform)
       s = xsg_vsum<G::LPR, real>(s);
@@ -1485,15 +1491,23 @@ __global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__res
         if (t != jb.nparts - 1) {
           mine = false;
         } else {
+          // the column's partial slots in chunk order, RB per subgroup in
+          // flight (sc1 buffer loads: the last-arriver hand-off), then a
+          // fixed tree over the subgroups: deterministic
           const uint32_t s0 = jb.slot - (jb.flags >> 1);
+          const BufView pv = buf_view(wpart, wbytes);
+          constexpr int RB = 8;
           vec_t<real> a = vzero<real>();
-          for (uint32_t q = sg; q < jb.nparts; q += G::NSG) {
-            vec_t<real> x;
+          for (uint32_t q0 = sg; q0 < jb.nparts; q0 += RB * G::NSG) {
+            vec_t<real> y[RB];
 #pragma unroll
-            for (int e = 0; e < G::VE; e++)
-              x[e] = __hip_atomic_load(wpart + (size_t)(s0 + q) * KP + li * G::VE + e, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            a += x;
+            for (int u = 0; u < RB; u++) {
+              const uint32_t q = q0 + u * G::NSG;
+              const uint32_t off = q < jb.nparts ? (uint32_t)(((size_t)(s0 + q) * KP + li * G::VE) * sizeof(real)) : pv.oob;
+              y[u] = __builtin_bit_cast(vec_t<real>, __builtin_amdgcn_raw_buffer_load_b128(pv.r, off, 0, 16));
+            }
+#pragma unroll
+            for (int u = 0; u < RB; u++) a += y[u];
           }
           s = xsg_vsum<G::LPR, real>(a);
           if (lane == 0) __hip_atomic_store(f.cnt + jb.col, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -239,16 +239,25 @@ static void build_csc(uint64_t R, uint64_t D, const int64_t *xptr, const uint32_
     if (cptr[d + 1] - cptr[d] <= (uint64_t)JOB_ENT && (!own || own[d]))
       jobs.push_back(Job{(uint32_t)d, 1u, 0u, 0u, (int64_t)cptr[d], (int64_t)cptr[d + 1]});
   while (jobs.size() % nsg) jobs.push_back(Job{JOB_NONE, 1u, 0u, 0u, 0, 0});
-  const uint64_t wc = (uint64_t)nsg * JOB_ENT;
   nslot = 0;
   for (uint64_t d = 0; d < D; d++) {
     const uint64_t b = cptr[d], e = cptr[d + 1];
     if (e - b <= (uint64_t)JOB_ENT || (own && !own[d])) continue;
+    // A heavy column of n entries: np wave-chunks, each subgroup walking R
+    // rounds of JOB_ENT entries, then the last chunk to arrive sums the np
+    // slots 8 per subgroup per round (kernels.hpp k_feat).  Both are chains
+    // of dependent load rounds, ~R and ~np / (8 nsg) long: with n = np R nsg
+    // JOB_ENT their sum is least at R = sqrt(K / (8 nsg)), K = n / (nsg
+    // JOB_ENT).  (A 400,000-row column: 632 chunks of 20 rounds instead of
+    // 12,500 one-round chunks summed 4 at a time.)
+    const double K = (double)(e - b) / ((double)nsg * JOB_ENT);
+    const uint64_t R = std::max<uint64_t>(1, (uint64_t)std::llround(std::sqrt(K / (8.0 * nsg))));
+    const uint64_t sub = (uint64_t)JOB_ENT * R, wc = (uint64_t)nsg * sub;
     const uint32_t np = (uint32_t)((e - b + wc - 1) / wc);
     for (uint32_t q = 0; q < np; q++)
       for (int g = 0; g < nsg; g++) {
-        const int64_t sb = (int64_t)std::min(e, b + q * wc + (uint64_t)g * JOB_ENT);
-        const int64_t se = (int64_t)std::min<uint64_t>(e, (uint64_t)sb + JOB_ENT);
+        const int64_t sb = (int64_t)std::min(e, b + q * wc + (uint64_t)g * sub);
+        const int64_t se = (int64_t)std::min<uint64_t>(e, (uint64_t)sb + sub);
         jobs.push_back(Job{(uint32_t)d, np, (uint32_t)(nslot + q), 1u | (q << 1), sb, se});
       }
     nslot += np;
@@ -1806,27 +1815,27 @@ template <typename real> class Problem final : public ProblemBase {
       const real *nq = nullptr;
       prof_launch(name, bytes, [&] {
         if (mode == 0) {
-          launch(k_feat<real, KP, 0>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, fin, nq);
+          launch(k_feat<real, KP, 0>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, wpart_.bytes(), fin, nq);
         } else if (mode == 1) {
           if constexpr ((size_t)KP * KP * sizeof(real) <= COLTAU_LDS) {
             if (coltau(h)) {
               fin.xsq = F.xsq.p;
               launch(k_feat<real, KP, 1, JOB_ENT, true>, grid, BLOCK, (size_t)KP * KP * sizeof(real), njw, jobs, crow,
-                     cval, h_.p, h_.bytes(), wpart_.p, fin, (const real *)qtq_);
+                     cval, h_.p, h_.bytes(), wpart_.p, wpart_.bytes(), fin, (const real *)qtq_);
               return;
             }
           }
-          launch(k_feat<real, KP, 1>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, fin, nq);
+          launch(k_feat<real, KP, 1>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, wpart_.bytes(), fin, nq);
         } else {
           if constexpr ((size_t)KP * KP * sizeof(real) <= COLTAU_LDS) {
             if (coltau(h) && it > 0) {
               fin.xsq = F.xsq.p;
               launch(k_feat<real, KP, 2, JOB_ENT, true>, grid, BLOCK, (size_t)KP * KP * sizeof(real), njw, jobs, crow,
-                     cval, h_.p, h_.bytes(), wpart_.p, fin, (const real *)qtq_);
+                     cval, h_.p, h_.bytes(), wpart_.p, wpart_.bytes(), fin, (const real *)qtq_);
               return;
             }
           }
-          launch(k_feat<real, KP, 2>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, fin, nq);
+          launch(k_feat<real, KP, 2>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, wpart_.bytes(), fin, nq);
         }
       });
     });

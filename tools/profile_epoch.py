@@ -1,5 +1,5 @@
-"""Per-kernel-family breakdown of kkbox-shape epochs (HIP events on the
-solver stream).  Usage: python tools/profile_epoch.py [fp32|fp64] [epochs]"""
+"""Per-kernel-family breakdown of epochs (HIP events on the solver stream).
+Usage: python tools/profile_epoch.py [fp32|fp64] [epochs] [kkbox|cfg5]"""
 import json
 import os
 import sys
@@ -15,8 +15,13 @@ import synth  # noqa: E402
 def main():
     prec = ocffm.FP64 if (len(sys.argv) > 1 and sys.argv[1] == "fp64") else ocffm.FP32
     epochs = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-    ds = synth.kkbox()
-    g = ocffm.problem_from_dataset(ds, precision=prec, with_test=False)
+    work = sys.argv[3] if len(sys.argv) > 3 else "kkbox"
+    if work == "cfg5":
+        ds = synth.cfg5(m=int(os.environ.get("CFG5_ROWS", "2000000")))
+        g = ocffm.problem_from_dataset(ds, precision=prec, with_test=False, k=64, self_side=False)
+    else:
+        ds = synth.kkbox()
+        g = ocffm.problem_from_dataset(ds, precision=prec, with_test=False)
     ocffm.srand(1)
     g.init()
     g.one_epoch()
@@ -41,7 +46,9 @@ def main():
     for name, v in rows:
         per = v["total_ms"] / max(1, v["launches"])
         bw = v["alg_bytes"] / max(1e-12, v["total_ms"] * 1e-3) / 1e9
-        print(f"{name:20s} {v['launches']/epochs:9.1f} {v['total_ms']/epochs:8.3f} {per*1e3:10.1f} {bw:9.1f}")
+        tf = v.get("alg_flops", 0.0) / max(1e-12, v["total_ms"] * 1e-3) / 1e12
+        print(f"{name:20s} {v['launches']/epochs:9.1f} {v['total_ms']/epochs:8.3f} {per*1e3:10.1f} {bw:9.1f}"
+              + (f" {tf:7.1f} TF/s" if tf else ""))
     out = os.path.join(REPO, "gpurun_out", "profile_epoch.json")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     json.dump({"plain_ms": plain * 1e3, "stats": ks, "epochs": epochs}, open(out, "w"), indent=1)

@@ -732,13 +732,34 @@ __global__ __launch_bounds__(TBLOCK) void k_rows_T(uint64_t R, int C, const floa
     for (int g0 = 0; g0 < C; g0 += TG) {
       const int ng = C - g0 < TG ? C - g0 : TG;
       __syncthreads();  // the previous stage's readers are done
-      for (int q = threadIdx.x; q < ng * KP * KP; q += TBLOCK) {
-        const int c = q / (KP * KP), rem = q % (KP * KP), k = rem / KP, col = rem % KP;
-        Ms[((c * KP + k) * 32 + (col & 31)) * NT + (col >> 5)] = M[(size_t)(g0 + c) * KP * KP + rem];
+      {
+        // the stage in one round of independent 16-B loads (up to TG KP^2 / 4
+        // / TBLOCK per thread), then the permuted LDS stores
+        // (in two halves: the staging registers are not live beside the
+        // operands' double buffer)
+        constexpr int PER = (TG * KP * KP / 4 + TBLOCK - 1) / TBLOCK, PH = PER / 2 > 0 ? PER / 2 : 1;
+        const BufView mb = buf_view(M + (size_t)g0 * KP * KP, (uint64_t)ng * KP * KP * 4);
+#pragma unroll 1
+        for (int u0 = 0; u0 < PER; u0 += PH) {
+          f4v mv[PH];
+#pragma unroll
+          for (int u = 0; u < PH; u++) mv[u] = bld<float>(mb, (uint32_t)(threadIdx.x + (u0 + u) * TBLOCK) * 16u);
+#pragma unroll
+          for (int u = 0; u < PH; u++) {
+            const int q = (threadIdx.x + (u0 + u) * TBLOCK) * 4;
+            if (q < ng * KP * KP) {
+              const int c = q / (KP * KP), rem = q % (KP * KP), k = rem / KP, col = rem % KP;
+#pragma unroll
+              for (int x = 0; x < 4; x++)
+                Ms[((c * KP + k) * 32 + ((col + x) & 31)) * NT + ((col + x) >> 5)] = mv[u][x];
+            }
+          }
+        }
       }
       __syncthreads();
       f4v a[2][TW][KH / 4];
-      auto load = [&](int sb, int c) {
+      auto load = [&](auto SB, int c) {
+        constexpr int sb = decltype(SB)::value;
         const BufView ab = buf_view(A[g0 + c], R * rowb);
 #pragma unroll
         for (int t = 0; t < TW; t++) {
@@ -748,10 +769,10 @@ __global__ __launch_bounds__(TBLOCK) void k_rows_T(uint64_t R, int C, const floa
           for (int q = 0; q < KH / 4; q++) a[sb][t][q] = bld<float>(ab, off + q * 16);
         }
       };
-      load(0, 0);
-      for (int c = 0; c < ng; c++) {
-        const int sb = c & 1;
-        if (c + 1 < ng) load(sb ^ 1, c + 1);
+      // table c on register set c % 2 (compile-time: a runtime set index
+      // would put the operands in scratch memory)
+      auto compute = [&](auto SB, int c) {
+        constexpr int sb = decltype(SB)::value;
         const float *mc = Ms + (size_t)c * KP * KP;
 #pragma unroll
         for (int s = 0; s < KH; s++) {
@@ -771,6 +792,14 @@ __global__ __launch_bounds__(TBLOCK) void k_rows_T(uint64_t R, int C, const floa
               acc[t][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[sb][t][s >> 2][s & 3], b, acc[t][0], 0, 0, 0);
           }
         }
+      };
+      load(std::integral_constant<int, 0>(), 0);
+      for (int c = 0; c < ng; c += 2) {
+        if (c + 1 < ng) load(std::integral_constant<int, 1>(), c + 1);
+        compute(std::integral_constant<int, 0>(), c);
+        if (c + 1 >= ng) break;
+        if (c + 2 < ng) load(std::integral_constant<int, 0>(), c + 2);
+        compute(std::integral_constant<int, 1>(), c + 1);
       }
     }
     // D register r of lane l: row 8(r/4) + 4(l/32) + r%4 of the tile, column l%32 (+32 n)
@@ -1996,7 +2025,7 @@ static __global__ __launch_bounds__(BLOCK) void k_gram_mfma64(uint64_t Rp, int C
                                                        float *__restrict__ part, uint64_t nout,
                                                        uint64_t rows_per_block, unsigned ngroups) {
   typedef float f16x __attribute__((ext_vector_type(16)));
-  constexpr int U = 4;  // row pairs per round
+  constexpr int U = 4;  // row pairs per round (U = 8: 9 % slower at config 5)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int e = lane & 31, hf = lane >> 5;
   const unsigned grp = blockIdx.x % ngroups, chunk = blockIdx.x / ngroups;

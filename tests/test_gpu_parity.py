@@ -422,6 +422,24 @@ def test_execution_variants_fp64(kk_small, monkeypatch, env):
     np.testing.assert_array_equal(g.cg_log(), o.cg_log())
 
 
+def test_unsorted_labels():
+    """Label lists in file order, not sorted (ffm.cpp:92-100 keeps them as
+    written): positives, their segments and both orientations of y~ follow
+    the file order (transY, ffm.cpp:259-294, sorts only by item)."""
+    ds = synth.tiny(seed=9)
+    rng = np.random.default_rng(1)
+    t = ds.train
+    for i in range(t.m):
+        b, e = int(t.yptr[i]), int(t.yptr[i + 1])
+        t.ycol[b:e] = rng.permutation(t.ycol[b:e])
+    o, g = pair(ds)
+    for _ in range(2):
+        o.one_epoch()
+        g.one_epoch()
+    assert_state(o, g, 1e-9)
+    np.testing.assert_array_equal(g.cg_log(), o.cg_log())
+
+
 def test_cold_rows_and_duplicate_labels():
     ds = synth.tiny(seed=6)
     # a test row whose features are all dropped -> popularity scores

@@ -26,7 +26,7 @@ def main():
             continue
         agpr = blk.split()[0]
         print(f"{name[:90]:90s} vgpr {get('vgpr_count'):>4} agpr {agpr:>4} sgpr {get('sgpr_count'):>4} "
-              f"spill {get('vgpr_spill_count')} lds {get('group_segment_fixed_size')}")
+              f"spill {get('vgpr_spill_count')} scratch {get('private_segment_fixed_size')} lds {get('group_segment_fixed_size')}")
 
 
 if __name__ == "__main__":

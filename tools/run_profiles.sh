@@ -13,16 +13,16 @@ out=gpurun_out
 sm=$out/summ_$tag
 mkdir -p $out $sm
 export TMPDIR=/tmp
-B="python bench.py --steps 5 --warmup 2 --cpu-baseline off"
+B="python bench.py --steps 5 --warmup 2 --cpu-baseline off --modes off --sgd off"
 S="python tools/bench_sgd.py --steps 3 --warmup 1 --cpu-sample 10"
 timeout -k 10 300 python bench.py > $out/bench_$tag.json 2> $out/bench_$tag.err
 timeout -k 10 300 python tools/bench_sgd.py > $out/bench_sgd_$tag.json 2> $out/bench_sgd_$tag.err
 rm -rf $out/prof_$tag $out/pmcf_$tag $out/pmcw_$tag $out/sprof_$tag $out/spmcf_$tag $out/spmcw_$tag
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof_$tag -o run -- $B > $out/prof_$tag.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmcf_$tag -o run \
-  -- python bench.py --steps 1 --warmup 1 --cpu-baseline off > $out/pmcf_$tag.log 2>&1
+  -- python bench.py --steps 1 --warmup 1 --cpu-baseline off --modes off --sgd off > $out/pmcf_$tag.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmcw_$tag -o run \
-  -- python bench.py --steps 1 --warmup 1 --cpu-baseline off > $out/pmcw_$tag.log 2>&1
+  -- python bench.py --steps 1 --warmup 1 --cpu-baseline off --modes off --sgd off > $out/pmcw_$tag.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/sprof_$tag -o run -- $S > $out/sprof_$tag.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_sgd --output-format csv -d $out/spmcf_$tag -o run \
   -- python tools/bench_sgd.py --steps 1 --warmup 0 --cpu-sample 10 > $out/spmcf_$tag.log 2>&1

@@ -378,8 +378,12 @@ __device__ __forceinline__ double block_sum(double v) {
 constexpr int TICK_SUB = 32;
 constexpr int TICK_STRIDE = 64;  // words
 constexpr int TICK_WORDS = (TICK_SUB + 1) * TICK_STRIDE;
+// extra (optional): nextra x NV more values, stored by waves of any block
+// before their block's ticket (sc1 stores, drained), added to the total in
+// index order by the last block.
 template <int NV>
-__device__ __forceinline__ bool last_block(const double (&v)[NV], double *part, unsigned *tick, double (&tot)[NV]) {
+__device__ __forceinline__ bool last_block(const double (&v)[NV], double *part, unsigned *tick, double (&tot)[NV],
+                                           const double *extra = nullptr, uint32_t nextra = 0) {
   __shared__ int s_last;
   if (threadIdx.x == 0) {
 #pragma unroll
@@ -423,6 +427,18 @@ __device__ __forceinline__ bool last_block(const double (&v)[NV], double *part, 
   }
 #pragma unroll
   for (int k = 0; k < NV; k++) tot[k] = block_sum(x[k]);
+  if (nextra) {  // the extra slots, thread-strided then the fixed block tree
+    const BufView ev = buf_view(extra, (uint64_t)nextra * NV * sizeof(double));
+    double y[NV];
+#pragma unroll
+    for (int k = 0; k < NV; k++) y[k] = 0;
+    for (uint32_t q = threadIdx.x; q < nextra; q += BLOCK)
+#pragma unroll
+      for (int k = 0; k < NV; k++)
+        y[k] += __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ev.r, (q * NV + k) * 8u, 0, 16));
+#pragma unroll
+    for (int k = 0; k < NV; k++) tot[k] += block_sum(y[k]);
+  }
   if (threadIdx.x == 0) __hip_atomic_store(tick, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
 }
@@ -476,6 +492,14 @@ template <typename real> struct Fin {
   // one-node-per-row field, summed per column: w (sum_{i in col} x_i^2) p QTQ
   const real *xsq;  // per column: sum of x^2 over its rows
   double tw;        // w
+  // Dot-product contributions of the columns a feature pass finalises in a
+  // last-arriving chunk (heavy columns, k_feat): one slot of 3 doubles per
+  // column (at its first chunk slot), summed by the grid's last block in
+  // slot order.  Which block finalises such a column depends on arrival
+  // order, so its terms must not enter that block's partial: the grid sum
+  // would then associate differently from run to run.  nhd: slots (0: none).
+  double *hdots;
+  uint32_t nhd;
 };
 
 // MODE 0 (gradient, ffm.cpp:561-570, 773-779): G = lam f W + s; r = -G;
@@ -583,7 +607,7 @@ __device__ __forceinline__ void cg_publish(const Fin<real> &f, const double (&to
 template <typename real, int MODE>
 __device__ __forceinline__ void fin_blocks(const Fin<real> &f, const double (&ds)[3]) {
   double bv[3] = {block_sum(ds[0]), block_sum(ds[1]), block_sum(ds[2])}, tot[3];
-  if (last_block<3>(bv, f.part, f.tick, tot) && threadIdx.x == 0) {
+  if (last_block<3>(bv, f.part, f.tick, tot, f.hdots, f.nhd) && threadIdx.x == 0) {
     if (f.dots) {
 #pragma unroll
       for (int k = 0; k < 3; k++) f.dots[k] = tot[k];
@@ -1503,6 +1527,7 @@ __global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__res
       b0 += JE;
     } while (b0 < jb.e);
     bool mine = jb.col != JOB_NONE;
+    int64_t hslot = -1;  // a last-arriving chunk: the column's dot-product slot
     if (jb.flags & 1u) {  // wave job (wave-uniform)
       s = xsg_vsum<G::LPR, real>(s);
       mine = sg == 0;
@@ -1539,6 +1564,7 @@ __global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__res
             for (int u = 0; u < RB; u++) a += y[u];
           }
           s = xsg_vsum<G::LPR, real>(a);
+          hslot = s0;
           if (lane == 0) __hip_atomic_store(f.cnt + jb.col, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
@@ -1550,9 +1576,22 @@ __global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__res
           s += vsplat<real>((real)(f.tw * (double)f.xsq[jb.col])) * sg_vecmat<real, KP>(d, Qs, li);
         }
         vst<real>(f.acc + (size_t)jb.col * KP + li * G::VE, s);
+      } else if (hslot >= 0 && f.hdots) {
+        // the column's dot products into its own slot (fixed order: the
+        // subgroup's lanes by DPP), not into this block's partial
+        double cd[3] = {0, 0, 0};
+        col_finalize<real, KP, (MODE == 2 ? 0 : MODE), TAU>(f, jb.col, s, alpha, beta, upd, li, cd, ops, Qs);
+#pragma unroll
+        for (int k = 0; k < 3; k++) cd[k] = sg_sum<G::LPR>(cd[k]);
+        if (li == 0)
+#pragma unroll
+          for (int k = 0; k < 3; k++)
+            __hip_atomic_store(f.hdots + (size_t)hslot * 3 + k, cd[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else col_finalize<real, KP, (MODE == 2 ? 0 : MODE), TAU>(f, jb.col, s, alpha, beta, upd, li, dsum, ops, Qs);
     }
   }
+  // the slot stores above are drained before this block's ticket (last_block)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (MODE != 2) fin_blocks<real, (MODE == 2 ? 0 : MODE)>(f, dsum);
 }
 
@@ -2020,7 +2059,7 @@ __global__ __launch_bounds__(BLOCK) void k_gram_mfma32(uint64_t Rp, const float 
 // Partials: part[chunk][c * 4096 + m * 64 + n] and, from group 0, wave 0,
 // the sums at [C * 4096 ..) (k_reduce_parts, fixed order).
 constexpr int GW64 = 1;  // tables per wave of k_gram_mfma64 (64 accumulators each)
-static __global__ __launch_bounds__(BLOCK) void k_gram_mfma64(uint64_t Rp, int C, const float *const *__restrict__ A,
+static __global__ __launch_bounds__(BLOCK, 3) void k_gram_mfma64(uint64_t Rp, int C, const float *const *__restrict__ A,
                                                        const float *__restrict__ B, const float *__restrict__ wv,
                                                        float *__restrict__ part, uint64_t nout,
                                                        uint64_t rows_per_block, unsigned ngroups) {

@@ -90,6 +90,7 @@ template <typename real> struct DevField {
   DevBuf<real> cval;
   DevBuf<Job> jobs;  // kernels.hpp: Job; njw waves of NSG jobs
   uint64_t njw = 0, nslot = 0;
+  DevBuf<double> hdots, shdots;  // heavy columns' dot-product slots (row / segment CSC; kernels.hpp Fin::hdots)
   DevBuf<real> freqw;  // global feature frequency (for --freq)
   DevBuf<real> xsq;    // one node per row: sum of x^2 over each column's rows (column tau)
   // the same CSC over positive segments (kernels.hpp: Seg) of the side
@@ -175,6 +176,7 @@ template <typename real> static void build_seg_csc(DevSide<real> &s, const std::
     F.scval.upload(cv);
     F.sjobs.upload(jobs);
     F.snjw = jobs.size() / nsg;
+    F.shdots.alloc(std::max<uint64_t>(F.snslot, 1) * 3);
     F.h_xptr.clear();
     F.h_xptr.shrink_to_fit();
     F.h_xidx.clear();
@@ -1007,6 +1009,7 @@ template <typename real> class Problem final : public ProblemBase {
       F->cval.upload(to_real(cval));
       F->jobs.upload(jobs);
       F->njw = jobs.size() / nsg();
+      F->hdots.alloc(std::max<uint64_t>(F->nslot, 1) * 3);
       F->cnt.alloc(std::max<uint64_t>(F->D, 1));
       if (F->one && !F->idlike && !F->excl && cgram_on_ && R > 0 && prm_.self_side && cgram_pays(R, F->D) &&
           F->D * kp_ * kp_ * sizeof(real) <= (1ull << 30))
@@ -1670,6 +1673,8 @@ template <typename real> class Problem final : public ProblemBase {
     f.dots = h.F->excl ? dots_.p : nullptr;
     f.xsq = nullptr;
     f.tw = w_;
+    f.hdots = nullptr;
+    f.nhd = 0;
     return f;
   }
   // Gram chunks of a one-node-per-row field (build_csc's column order): each
@@ -1808,6 +1813,8 @@ template <typename real> class Problem final : public ProblemBase {
                            (double)h.D * KP * rs * vecs;
       const unsigned grid = (unsigned)std::min<uint64_t>((njw + 3) / 4, feat_blocks_);  // grid-stride: fewer tickets
       Fin<real> fin = make_fin(h, it);
+      fin.hdots = seg ? F.shdots.p : F.hdots.p;
+      fin.nhd = (uint32_t)(seg ? F.snslot : F.nslot);
       const Job *jobs = seg ? F.sjobs.p : F.jobs.p;
       const uint32_t *crow = seg ? F.scrow.p : F.crow.p;
       const real *cval = seg ? F.scval.p : F.cval.p;
@@ -2136,6 +2143,7 @@ template <typename real> class Problem final : public ProblemBase {
   double w_, lam_, r_;
   uint64_t m_glob_ = 0, n_ = 0, u0_ = 0, u1_ = 0, dmax_ = 0, npop_ = 0;
   uint64_t seg_len_ = 32;
+
   int lookahead_ = 1;
   // speculative update at the previous epoch's CG count (OCFFM_SPEC=0: off)
   bool spec_on_ = !std::getenv("OCFFM_SPEC") || std::atoi(std::getenv("OCFFM_SPEC")) != 0;

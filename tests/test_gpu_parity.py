@@ -347,27 +347,33 @@ def test_heavy_columns(precision, cgram, monkeypatch):
         assert abs(gpu_objective(o2, g) - f_ref) <= 1e-3 * abs(f_ref)
 
 
-@pytest.mark.parametrize("ds_name", ["heavy", "kkbox_s", "kkbox_s_cgram2"])
+@pytest.mark.parametrize("ds_name", ["heavy", "kkbox_s", "kkbox_s_cgram2", "cfg5", "cfg5_k32", "cfg5_nomfma"])
 def test_fp32_runs_bit_identical(ds_name, monkeypatch):
     """The default fp32 path has no order-dependent float sums (feature
     passes, Gram builds and grid reductions combine in a fixed order): two
     runs of the same epochs give bit-identical tables and CG logs.  "heavy"
     forces the Gram path onto multi-chunk columns (k_col_gram's partial slots)."""
+    kw = {}
     if ds_name == "heavy":
         monkeypatch.setenv("OCFFM_CGRAM", "2")
         ds = synth.general(**HEAVY)
+    elif ds_name.startswith("cfg5"):  # MFMA T pre-pass and KP = 64 Grams, heavy columns
+        ds = synth.cfg5(m=20000, n=3000, d_user=2000, seed=3)
+        kw = dict(k=32 if ds_name.endswith("k32") else 64, self_side=False)
+        if ds_name.endswith("nomfma"):
+            monkeypatch.setenv("OCFFM_NO_MFMA", "1")
     else:
         if ds_name.endswith("cgram2"):  # MFMA per-column Grams (k = 32), multi-chunk slot sums
             monkeypatch.setenv("OCFFM_CGRAM", "2")
         ds = synth.kkbox(m=3000, n=4000, mean=20.0, seed=11, name="kk_det")
     runs = []
     for _ in range(2):
-        g = ocffm.problem_from_dataset(ds, precision=ocffm.FP32, with_test=False)
+        g = ocffm.problem_from_dataset(ds, precision=ocffm.FP32, with_test=False, **kw)
         ocffm.srand(1)
         g.init()
         for _ in range(2):
             g.one_epoch()
-        o = O.Oracle(ds, with_test=False)  # only for the block list
+        o = O.Oracle(ds, with_test=False, **kw)  # only for the block list
         runs.append(([g.get(w, b) for b in state_names(o) for w in "WH"], g.cg_log().copy()))
         g.close()
     for a, b in zip(runs[0][0], runs[1][0]):

@@ -7,7 +7,7 @@ tag=$1; shift
 out=gpurun_out
 mkdir -p $out
 export TMPDIR=/tmp
-eval "timeout -k 10 900 python -u -m pytest $1 -x -v --timeout 300 --timeout-method thread" > $out/pytest_$tag.log 2>&1
+eval "timeout -k 10 900 python -u -m pytest $1 ${PYX--x} -v --timeout 300 --timeout-method thread" > $out/pytest_$tag.log 2>&1
 shift
 if [ "$1" = smoke ]; then
   timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke_$tag.log 2>&1

@@ -220,6 +220,14 @@ int ocffm_problem_reset_stats(ocffm_problem *p);
  * (SURVEY §8d formula with the actual CG counts). */
 int ocffm_problem_alg_bytes(ocffm_problem *p, double *bytes);
 int ocffm_problem_sync(ocffm_problem *p);
+/* Digests (FNV-1a over the bytes) of every array of the device data layout
+ * the problem built from its ImpData (per-field CSR of split_fields,
+ * ffm.cpp:185-257; the item-major positives of transY, ffm.cpp:259-294; the
+ * popularity, ffm.cpp:143,172-176; the CSCs, jobs and segments), in a fixed
+ * order.  The layout is built on the device unless OCFFM_HOST_BUILD=1 was
+ * set at create; both builds give the same digests.  names: cap x 48 chars
+ * (may be NULL); *count receives the number of entries. */
+int ocffm_problem_layout_digest(ocffm_problem *p, char *names, uint64_t *digests, int cap, int *count);
 void ocffm_problem_destroy(ocffm_problem *p);
 
 /* ------------------------------------------------------------ SGD mode

@@ -253,8 +253,11 @@ Rows parse_rows(const std::string &path, bool has_label, const uint64_t *ds, uin
   return r;
 }
 
-// split_fields (ffm.cpp:185-257) + popularity (ffm.cpp:143,172-176).
-void build(HostData &d, const Rows &r) {
+// The row-level part of ImpData::read / split_fields: m, f, n, nnx, the
+// labels and Ds (ffm.cpp:126-181, 221), by one pass over the nodes cut
+// among host threads.  The per-field split itself is deferred: the device
+// build (devbuild.h) does it, or split_host when a host consumer asks.
+void build(HostData &d, Rows &&r) {
   d.has_label = r.has_label;
   d.m = r.xptr.size() - 1;
   d.f = r.f;
@@ -262,21 +265,55 @@ void build(HostData &d, const Rows &r) {
   d.nnx.resize(d.m);
   for (uint64_t i = 0; i < d.m; i++) d.nnx[i] = r.xptr[i + 1] - r.xptr[i];
   if (r.has_label) {
-    d.yptr = r.yptr;
-    d.ycol = r.ycol;
+    d.yptr = std::move(r.yptr);
+    d.ycol = std::move(r.ycol);
+  } else {
+    d.yptr.assign(d.m + 1, 0);
+    d.ycol.clear();
+  }
+  r.yptr.assign(1, 0);
+  r.ycol.clear();
+  const uint64_t nn = r.fid.size(), f = d.f;
+  const unsigned hw = std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
+  const unsigned nth = nn < (1u << 20) ? 1u : hw;
+  std::vector<std::vector<uint64_t>> ds(nth, std::vector<uint64_t>(f, 0));
+  std::vector<char> bad(nth, 0);
+  auto work = [&](unsigned t) {
+    const uint64_t a = nn * t / nth, b = nn * (t + 1) / nth;
+    std::vector<uint64_t> &m = ds[t];
+    for (uint64_t p = a; p < b; p++) {
+      const uint64_t x = r.idx[p];
+      if (x >= (1ULL << 32) - 1) bad[t] = 1;
+      m[r.fid[p]] = std::max<uint64_t>(m[r.fid[p]], x + 1);
+    }
+  };
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < nth; t++) th.emplace_back(work, t);
+  work(0);
+  for (auto &x : th) x.join();
+  for (char b : bad)
+    if (b) throw std::runtime_error("feature index exceeds 2^32-2");
+  d.Ds.assign(f, 0);
+  for (auto &m : ds)
+    for (uint64_t fi = 0; fi < f; fi++) d.Ds[fi] = std::max(d.Ds[fi], m[fi]);
+  d.raw = std::move(r);
+}
+
+// split_fields (ffm.cpp:185-257) + popularity (ffm.cpp:143,172-176) on the
+// host: the checker of the device build and the input of the host consumers.
+const HostData &split_host(const HostData &d) {
+  if (d.split_done) return d;
+  const Rows &r = d.raw;
+  if (d.has_label) {
     d.popular.assign(d.n, 0.0);
     for (uint64_t j : d.ycol) d.popular[j] += 1;
     double s = 0;
     for (double v : d.popular) s += v;
     for (double &v : d.popular) v /= s;
-  } else {
-    d.yptr.assign(d.m + 1, 0);
-    d.ycol.clear();
   }
   d.xptr.assign(d.f, std::vector<int64_t>(d.m + 1, 0));
   d.xidx.assign(d.f, {});
   d.xval.assign(d.f, {});
-  d.Ds.assign(d.f, 0);
   for (uint64_t i = 0; i < d.m; i++)
     for (uint64_t p = r.xptr[i]; p < r.xptr[i + 1]; p++) d.xptr[r.fid[p]][i + 1]++;
   for (uint64_t fi = 0; fi < d.f; fi++) {
@@ -288,29 +325,21 @@ void build(HostData &d, const Rows &r) {
   for (uint64_t i = 0; i < d.m; i++)
     for (uint64_t p = r.xptr[i]; p < r.xptr[i + 1]; p++) {
       const uint32_t fi = r.fid[p];
-      if (r.idx[p] >= (1ULL << 32) - 1) throw std::runtime_error("feature index exceeds 2^32-2");
       const uint64_t q = cur[fi]++;
       d.xidx[fi][q] = (uint32_t)r.idx[p];
       d.xval[fi][q] = r.val[p];
-      d.Ds[fi] = std::max<uint64_t>(d.Ds[fi], r.idx[p] + 1);
     }
+  d.split_done = true;
+  return d;
 }
 
-// ffm.cpp:259-294.  Labels >= #items are skipped here like the reference;
-// the problem constructor rejects them (the reference reads out of bounds).
+// ffm.cpp:259-294.  The item-major positives themselves are built by the
+// problem (solver.hip build_item_side: on the device, or on the host with
+// OCFFM_HOST_BUILD=1), restricted to its rank's users; here only the
+// pairing is recorded.  Labels >= #items: the reference skips them in
+// transY and then reads out of bounds; the problem constructor rejects them.
 void trans_y(HostData &V, const HostData &U) {
-  std::vector<uint64_t> cnt(V.m + 1, 0);
-  for (uint64_t p = 0; p < U.ycol.size(); p++)
-    if (U.ycol[p] < V.m) cnt[U.ycol[p] + 1]++;
-  for (uint64_t j = 0; j < V.m; j++) cnt[j + 1] += cnt[j];
-  V.tptr = cnt;
-  V.tcol.assign(cnt[V.m], 0);
-  std::vector<uint64_t> cur(cnt.begin(), cnt.end() - 1);
-  for (uint64_t i = 0; i < U.m; i++)
-    for (uint64_t p = U.yptr[i]; p < U.yptr[i + 1]; p++) {
-      const uint64_t j = U.ycol[p];
-      if (j < V.m) V.tcol[cur[j]++] = (uint32_t)i;
-    }
+  (void)U;
   V.transposed = true;
 }
 

@@ -563,8 +563,9 @@ class Trainer {
     return a;
   }
   // Row node lists (field-major within a row, file order within a field).
-  void build_nodes(const HostData &D, uint32_t fbase, const std::vector<uint64_t> &off, DevBuf<uint64_t> &ptr,
+  void build_nodes(const HostData &Draw, uint32_t fbase, const std::vector<uint64_t> &off, DevBuf<uint64_t> &ptr,
                    DevBuf<uint32_t> &node, DevBuf<uint32_t> &fld, DevBuf<float> &val, int &nmax) {
+    const HostData &D = split_host(Draw);
     std::vector<uint64_t> p(D.m + 1, 0);
     std::vector<uint32_t> nd, fd;
     std::vector<float> vl;

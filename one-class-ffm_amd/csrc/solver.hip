@@ -32,6 +32,7 @@
 
 #include "../../include/ocffm.h"
 #include "common.hpp"
+#include "devbuild.h"
 #include "host_data.h"
 #include "kernels.hpp"
 
@@ -72,6 +73,11 @@ static unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap = 4096
   if (g < 1) g = 1;
   if (g > cap) g = cap;
   return (unsigned)g;
+}
+
+template <typename real> __global__ void k_to_real(uint64_t n, const double *__restrict__ in, real *__restrict__ out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = (real)in[i];
 }
 
 // -------------------------------------------------------------- profiling
@@ -252,8 +258,8 @@ static void build_csc(uint64_t R, uint64_t D, const int64_t *xptr, const uint32_
     // JOB_ENT their sum is least at R = sqrt(K / (8 nsg)), K = n / (nsg
     // JOB_ENT).  (A 400,000-row column: 632 chunks of 20 rounds instead of
     // 12,500 one-round chunks summed 4 at a time.)
-    const double K = (double)(e - b) / ((double)nsg * JOB_ENT);
-    const uint64_t R = std::max<uint64_t>(1, (uint64_t)std::llround(std::sqrt(K / (8.0 * nsg))));
+    // (R = round(sqrt(K / (8 nsg))) in integers: devbuild.h heavy_rounds)
+    const uint64_t R = dev::heavy_rounds(e - b, nsg);
     const uint64_t sub = (uint64_t)JOB_ENT * R, wc = (uint64_t)nsg * sub;
     const uint32_t np = (uint32_t)((e - b + wc - 1) / wc);
     for (uint32_t q = 0; q < np; q++)
@@ -282,6 +288,7 @@ struct ProblemBase {
   virtual void save_binary(const std::string &path) = 0;
   virtual void load_binary(const std::string &path) = 0;
   virtual void sync() = 0;
+  virtual std::vector<std::pair<std::string, uint64_t>> layout_digest() = 0;
   virtual bool has_test() const = 0;
   virtual uint32_t nr_pass() const = 0;
   virtual int rank() const = 0;
@@ -330,14 +337,21 @@ template <typename real> class Problem final : public ProblemBase {
     u0_ = U.m * (uint64_t)comm_.rank / (uint64_t)comm_.nranks;
     u1_ = U.m * (uint64_t)(comm_.rank + 1) / (uint64_t)comm_.nranks;
     tmark(nullptr);
-    build_user_side(U);
-    tmark("create: user side");
-    build_item_side(V, U);
-    tmark("create: item side");
-    if (Ut) build_test(*Ut, U);
-    tmark("create: test rows");
-    popular_.upload(U.popular);
-    npop_ = U.popular.size();
+    {
+      // the data layout: built on the device (devbuild.h), or on the host
+      // with OCFFM_HOST_BUILD=1 (the checker: identical arrays)
+      dev::Builder B(stream_);
+      build_user_side(U, B);
+      tmark("create: user side");
+      build_item_side(V, U, B);
+      tmark("create: item side");
+      if (Ut) build_test(*Ut, U, B);
+      tmark("create: test rows");
+      if (host_build_) popular_.upload(split_host(U).popular);
+      else B.popularity(U, popular_);
+      npop_ = U.has_label ? U.n : 0;
+      B.sync();
+    }
     blocks_.resize(f_ * (f_ + 1) / 2);
     W_.resize(blocks_.size());
     H_.resize(blocks_.size());
@@ -407,6 +421,71 @@ template <typename real> class Problem final : public ProblemBase {
   uint32_t nr_pass() const override { return prm_.nr_pass; }
   int rank() const override { return comm_.rank; }
   void sync() override { HIPCHK(hipStreamSynchronize(stream_)); }
+
+  // FNV-1a digests of every array of the data layout (and its counts), in
+  // a fixed order: the device build and the host build must agree on each.
+  std::vector<std::pair<std::string, uint64_t>> layout_digest() override {
+    sync();
+    std::vector<std::pair<std::string, uint64_t>> out;
+    auto fnv = [](const void *p, size_t n, uint64_t h) {
+      const unsigned char *b = (const unsigned char *)p;
+      for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 0x100000001b3ull;
+      return h;
+    };
+    auto num = [&](const std::string &name, uint64_t v) { out.emplace_back(name, fnv(&v, sizeof(v), 0xcbf29ce484222325ull)); };
+    auto buf = [&](const std::string &name, const auto &b) {
+      using T = std::remove_pointer_t<decltype(b.p)>;
+      std::vector<T> h(b.n);
+      if (b.n) HIPCHK(hipMemcpy(h.data(), b.p, b.n * sizeof(T), hipMemcpyDeviceToHost));
+      out.emplace_back(name, fnv(h.data(), h.size() * sizeof(T), fnv(&b.n, sizeof(b.n), 0xcbf29ce484222325ull)));
+    };
+    const char *sn[3] = {"U", "V", "T"};
+    DevSide<real> *sd[3] = {&U_, &V_, &T_};
+    for (int q = 0; q < 3; q++) {
+      DevSide<real> &s = *sd[q];
+      const std::string p = sn[q];
+      num(p + ".R", s.R);
+      num(p + ".npos", s.npos);
+      num(p + ".nseg", s.nseg);
+      buf(p + ".yptr", s.yptr);
+      buf(p + ".ycol", s.ycol);
+      buf(p + ".perm", s.perm);
+      buf(p + ".segs", s.segs);
+      buf(p + ".segptr", s.segptr);
+      for (size_t fi = 0; fi < s.F.size(); fi++) {
+        DevField<real> &F = *s.F[fi];
+        const std::string f = p + ".F" + std::to_string(fi) + ".";
+        num(f + "D", F.D);
+        num(f + "nnz", F.nnz);
+        num(f + "flags", (F.one ? 1 : 0) | (F.idlike ? 2 : 0) | (F.excl ? 4 : 0));
+        num(f + "njw", F.njw);
+        num(f + "nslot", F.nslot);
+        num(f + "snjw", F.snjw);
+        num(f + "snslot", F.snslot);
+        num(f + "gslots", F.gslots);
+        buf(f + "xptr", F.xptr);
+        buf(f + "xidx", F.xidx);
+        buf(f + "xval", F.xval);
+        buf(f + "crow", F.crow);
+        buf(f + "cval", F.cval);
+        buf(f + "jobs", F.jobs);
+        buf(f + "scrow", F.scrow);
+        buf(f + "scval", F.scval);
+        buf(f + "sjobs", F.sjobs);
+        buf(f + "segd", F.segd);
+        buf(f + "segx", F.segx);
+        buf(f + "xsq", F.xsq);
+        buf(f + "freqw", F.freqw);
+        buf(f + "gchunks", F.gchunks);
+        buf(f + "gsums", F.gsums);
+        buf(f + "own", F.own);
+      }
+    }
+    buf("popular", popular_);
+    buf("gvptr", gvptr_);
+    num("npop", npop_);
+    return out;
+  }
 
   // --------------------------------------------------------------- init
   // ffm.cpp:467-512.
@@ -941,31 +1020,115 @@ template <typename real> class Problem final : public ProblemBase {
 
  private:
   // ------------------------------------------------------------ setup
-  // Owned field test over the contiguous row shards of all ranks (every rank
-  // holds the whole HostData, so no communication is needed).
-  void ownership(DevField<real> &F, const HostData &d, uint64_t fi) {
-    const uint64_t m = d.m, N = (uint64_t)comm_.nranks;
-    std::vector<int32_t> who(F.D, -1);
-    bool excl = true;
-    for (uint64_t q = 0; q < N && excl; q++) {
+  // Owned-field test over the contiguous row shards of all ranks (every rank
+  // holds the whole HostData, so no communication is needed): per field, the
+  // rank whose rows touch each feature (-1: none, -2: several), from one
+  // pass over the parsed nodes.
+  std::vector<std::vector<int32_t>> owners(const HostData &d, const std::vector<uint64_t> &Ds) {
+    const Rows &r = d.raw;
+    const uint64_t m = d.m, N = (uint64_t)comm_.nranks, nf = Ds.size();
+    std::vector<std::vector<int32_t>> who(nf);
+    for (uint64_t f = 0; f < nf; f++) who[f].assign(Ds[f], -1);
+    for (uint64_t q = 0; q < N; q++) {
       const uint64_t a = m * q / N, b = m * (q + 1) / N;
-      for (int64_t p = d.xptr[fi][a]; p < d.xptr[fi][b] && excl; p++) {
-        int32_t &w = who[d.xidx[fi][p]];
-        if (w < 0) w = (int32_t)q;
-        else if (w != (int32_t)q) excl = false;
+      for (uint64_t p = r.xptr[a]; p < r.xptr[b]; p++) {
+        if (r.fid[p] >= nf) continue;
+        int32_t &w = who[r.fid[p]][r.idx[p]];
+        if (w == -1) w = (int32_t)q;
+        else if (w != (int32_t)q) w = -2;
       }
     }
-    if (!excl || no_owned_) return;
+    return who;
+  }
+  void ownership(DevField<real> &F, const std::vector<int32_t> &who) {
+    if (no_owned_ || std::find(who.begin(), who.end(), -2) != who.end()) return;
     F.excl = true;
     F.h_own.resize(F.D);
     for (uint64_t x = 0; x < F.D; x++) F.h_own[x] = who[x] == comm_.rank || (who[x] < 0 && comm_.rank == 0);
     F.own.upload(F.h_own);
   }
+  // --freq on several ranks: each field's feature counts over all rows.
+  std::vector<std::vector<double>> global_counts(const HostData &d, const std::vector<uint64_t> &Ds) {
+    const Rows &r = d.raw;
+    std::vector<std::vector<double>> c(Ds.size());
+    for (size_t f = 0; f < Ds.size(); f++) c[f].assign(Ds[f], 0.0);
+    for (uint64_t p = 0; p < r.fid.size(); p++)
+      if (r.fid[p] < Ds.size()) c[r.fid[p]][r.idx[p]] += 1;
+    return c;
+  }
+  // Side halves of this one-node field run on per-column Grams.
+  bool gram_field(const DevField<real> &F, uint64_t R) const {
+    return F.one && !F.idlike && !F.excl && cgram_on_ && R > 0 && prm_.self_side && cgram_pays(R, F.D) &&
+           F.D * kp_ * kp_ * sizeof(real) <= (1ull << 30);
+  }
 
-  void build_fields(DevSide<real> &s, const HostData &d, uint64_t r0, uint64_t r1,
-                    const std::vector<uint64_t> &Ds_glob, bool owned = false) {
+  // Per-field CSR, CSC + jobs, flags and column sums of rows [r0, r1) of d
+  // (split_fields, ffm.cpp:185-257, and the layout of DESIGN §5), on the
+  // device (devbuild.h); OCFFM_HOST_BUILD=1: on the host.  Returns (device
+  // build) each field's fp64 node values, which the segment CSCs read.
+  std::vector<DevBuf<double>> build_fields(DevSide<real> &s, const HostData &d, uint64_t r0, uint64_t r1,
+                                           const std::vector<uint64_t> &Ds_glob, dev::Builder &B, bool owned = false) {
     s.F.clear();
     s.Ds = Ds_glob;
+    const uint64_t R = r1 - r0;
+    const uint32_t nf = (uint32_t)Ds_glob.size();
+    std::vector<std::vector<int32_t>> who;
+    if (owned) who = owners(d, Ds_glob);
+    std::vector<std::vector<double>> gcnt;
+    if (prm_.freq && comm_.nranks > 1) gcnt = global_counts(d, Ds_glob);
+    if (host_build_) {
+      build_fields_host(s, split_host(d), r0, r1, Ds_glob, who, gcnt);
+      return {};
+    }
+    std::vector<dev::CSR> csr = B.split(d, r0, r1, nf);
+    tmark("create:   split_fields");
+    std::vector<DevBuf<double>> vals(nf);
+    for (uint32_t fi = 0; fi < nf; fi++) {
+      auto F = std::make_unique<DevField<real>>();
+      F->D = Ds_glob[fi];
+      dev::CSR &x = csr[fi];
+      F->nnz = x.nnz;
+      if (owned && fi < d.f) ownership(*F, who[fi]);
+      dev::CSC c;
+      B.csc(x, F->D, nsg(), F->excl ? F->own.p : nullptr, c);
+      B.flags(x, c, F->D, F->one, F->idlike);
+      F->xptr = std::move(x.xptr);
+      F->xidx = std::move(x.xidx);
+      to_real_dev(x.xval.p, x.nnz, F->xval);
+      if (F->one) to_real_dev(B.xsq(c, F->D), std::max<uint64_t>(F->D, 1), F->xsq);
+      F->crow = std::move(c.crow);
+      to_real_dev(c.cval, F->nnz, F->cval);
+      F->jobs = std::move(c.jobs);
+      F->njw = c.njobs / nsg();
+      F->nslot = c.nslot;
+      F->hdots.alloc(std::max<uint64_t>(F->nslot, 1) * 3);
+      F->cnt.alloc(std::max<uint64_t>(F->D, 1));
+      if (gram_field(*F, R)) {
+        std::vector<int64_t> cptr(F->D + 1);
+        HIPCHK(hipMemcpyAsync(cptr.data(), c.cptr, cptr.size() * sizeof(int64_t), hipMemcpyDeviceToHost, stream_));
+        B.sync();
+        col_gram_chunks(*F, cptr);
+      }
+      if (prm_.freq && fi < d.f) {
+        if (comm_.nranks > 1) {
+          F->freqw.upload(to_real(gcnt[fi]));
+        } else {
+          to_real_dev(B.col_counts(c, F->D), F->D, F->freqw);
+        }
+      }
+      B.sync();  // (c's buffers are freed at the end of the iteration)
+      vals[fi] = std::move(x.xval);
+      s.F.push_back(std::move(F));
+    }
+    tmark("create:   CSCs + jobs");
+    return vals;
+  }
+
+  // The host build: the reference's loops restated (the checker of the
+  // device build, OCFFM_HOST_BUILD=1).
+  void build_fields_host(DevSide<real> &s, const HostData &d, uint64_t r0, uint64_t r1,
+                         const std::vector<uint64_t> &Ds_glob, const std::vector<std::vector<int32_t>> &who,
+                         const std::vector<std::vector<double>> &gcnt) {
     const uint64_t R = r1 - r0;
     for (uint64_t fi = 0; fi < Ds_glob.size(); fi++) {
       auto F = std::make_unique<DevField<real>>();
@@ -991,55 +1154,98 @@ template <typename real> class Problem final : public ProblemBase {
         }
         F->idlike = ok;
       }
-      if (owned && fi < d.f) ownership(*F, d, fi);
+      if (!who.empty() && fi < d.f) ownership(*F, who[fi]);
       F->xptr.upload(xptr);
       F->xidx.upload(xidx);
       F->xval.upload(to_real(xval));
-      if (F->one) {
-        std::vector<double> sq(std::max<uint64_t>(F->D, 1), 0.0);
-        for (uint64_t i = 0; i < R; i++) sq[xidx[i]] += xval[i] * xval[i];
-        F->xsq.upload(to_real(sq));
-      }
       std::vector<uint32_t> crow;
       std::vector<double> cval;
       std::vector<Job> jobs;
       build_csc(R, F->D, xptr.data(), xidx.data(), xval.data(), nsg(), crow, cval, jobs, F->nslot,
                 F->excl ? F->h_own.data() : nullptr);
+      if (F->one) {  // sum of x^2 per column, rows in order (devbuild.h xsq_col)
+        std::vector<uint64_t> cptr(F->D + 1, 0);
+        for (uint32_t c : xidx) cptr[c + 1]++;
+        for (uint64_t q = 0; q < F->D; q++) cptr[q + 1] += cptr[q];
+        std::vector<double> sq(std::max<uint64_t>(F->D, 1), 0.0);
+        for (uint64_t q = 0; q < F->D; q++) sq[q] = dev::xsq_col(cval.data() + cptr[q], cptr[q + 1] - cptr[q]);
+        F->xsq.upload(to_real(sq));
+      }
       F->crow.upload(crow);
       F->cval.upload(to_real(cval));
       F->jobs.upload(jobs);
       F->njw = jobs.size() / nsg();
       F->hdots.alloc(std::max<uint64_t>(F->nslot, 1) * 3);
       F->cnt.alloc(std::max<uint64_t>(F->D, 1));
-      if (F->one && !F->idlike && !F->excl && cgram_on_ && R > 0 && prm_.self_side && cgram_pays(R, F->D) &&
-          F->D * kp_ * kp_ * sizeof(real) <= (1ull << 30))
-        col_gram_chunks(*F, xidx);
+      if (gram_field(*F, R)) {
+        std::vector<int64_t> cptr(F->D + 1, 0);
+        for (uint32_t c : xidx) cptr[c + 1]++;
+        for (uint64_t q = 0; q < F->D; q++) cptr[q + 1] += cptr[q];
+        col_gram_chunks(*F, cptr);
+      }
       F->h_xptr = std::move(xptr);
       F->h_xidx = std::move(xidx);
       F->h_xval = std::move(xval);
       if (prm_.freq && fi < d.f) {  // global counts (all rows, not just this shard)
-        std::vector<double> fr(F->D, 0.0);
-        for (uint32_t x : d.xidx[fi]) fr[x] += 1;
-        F->freqw.upload(to_real(fr));
+        if (!gcnt.empty()) {
+          F->freqw.upload(to_real(gcnt[fi]));
+        } else {
+          std::vector<double> fr(F->D, 0.0);
+          for (uint32_t x : d.xidx[fi]) fr[x] += 1;
+          F->freqw.upload(to_real(fr));
+        }
       }
       s.F.push_back(std::move(F));
     }
   }
 
-  void build_user_side(const HostData &U) {
+  // Segments and the segment CSCs of a side on the device (the host build:
+  // build_segments).  vals: each field's fp64 node values (build_fields).
+  void build_segments_dev(DevSide<real> &s, const DevBuf<int64_t> &yptr, uint64_t R, std::vector<DevBuf<double>> &vals,
+                          dev::Builder &B) {
+    B.segments(yptr.p, R, seg_len_, s.segs, s.segptr, s.nseg);
+    for (size_t fi = 0; fi < s.F.size(); fi++) {
+      DevField<real> &F = *s.F[fi];
+      const dev::CSR &ex = B.seg_expand(F.xptr.p, F.xidx.p, vals[fi].p, s.segs.p, s.nseg);
+      if (F.one) {  // one node per segment
+        F.segd.alloc(ex.nnz, false);
+        if (ex.nnz)
+          HIPCHK(hipMemcpyAsync(F.segd.p, ex.xidx.p, ex.nnz * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream_));
+        to_real_dev(ex.xval.p, ex.nnz, F.segx);
+      }
+      dev::CSC c;
+      B.csc(ex, F.D, nsg(), F.excl ? F.own.p : nullptr, c);
+      F.scrow = std::move(c.crow);
+      to_real_dev(c.cval, ex.nnz, F.scval);
+      F.sjobs = std::move(c.jobs);
+      F.snjw = c.njobs / nsg();
+      F.snslot = c.nslot;
+      F.shdots.alloc(std::max<uint64_t>(F.snslot, 1) * 3);
+      B.sync();
+      vals[fi].release();
+    }
+  }
+
+  void build_user_side(const HostData &U, dev::Builder &B) {
     U_.R = u1_ - u0_;
     U_.R_glob = U.m;
     U_.row0 = u0_;
-    build_fields(U_, U, u0_, u1_, U.Ds, comm_.nranks > 1);
+    auto vals = build_fields(U_, U, u0_, u1_, U.Ds, B, comm_.nranks > 1);
     const uint64_t pb = U.yptr[u0_], pe = U.yptr[u1_];
-    std::vector<int64_t> yptr(U_.R + 1);
-    for (uint64_t i = 0; i <= U_.R; i++) yptr[i] = (int64_t)(U.yptr[u0_ + i] - pb);
-    std::vector<uint32_t> ycol(pe - pb);
-    for (uint64_t p = pb; p < pe; p++) ycol[p - pb] = (uint32_t)U.ycol[p];
     U_.npos = pe - pb;
-    build_segments(U_, yptr, seg_len_, nsg());
-    U_.yptr.upload(yptr);
-    U_.ycol.upload(ycol);
+    if (host_build_) {
+      std::vector<int64_t> yptr(U_.R + 1);
+      for (uint64_t i = 0; i <= U_.R; i++) yptr[i] = (int64_t)(U.yptr[u0_ + i] - pb);
+      std::vector<uint32_t> ycol(pe - pb);
+      for (uint64_t p = pb; p < pe; p++) ycol[p - pb] = (uint32_t)U.ycol[p];
+      build_segments(U_, yptr, seg_len_, nsg());
+      U_.yptr.upload(yptr);
+      U_.ycol.upload(ycol);
+    } else {
+      B.labels(U, u0_, u1_, U_.yptr, U_.ycol);
+      build_segments_dev(U_, U_.yptr, U_.R, vals, B);
+      tmark("create:   segments + CSCs");
+    }
     U_.yt.alloc(std::max<uint64_t>(U_.npos, 1));
     U_.bias.alloc(std::max<uint64_t>(U_.R, 1));
     U_.s.alloc(std::max<uint64_t>(U_.R, 1));
@@ -1048,70 +1254,100 @@ template <typename real> class Problem final : public ProblemBase {
   // Item-major positives restricted to this rank's users, and the position
   // maps between the two orientations (transY order: users increasing,
   // labels in file order, ffm.cpp:259-294).
-  void build_item_side(const HostData &V, const HostData &U) {
+  void build_item_side(const HostData &V, const HostData &U, dev::Builder &B) {
     V_.R = V.m;
     V_.R_glob = V.m;
     V_.row0 = 0;
-    build_fields(V_, V, 0, V.m, V.Ds);
-    std::vector<int64_t> vptr(V.m + 1, 0);
-    for (uint64_t i = u0_; i < u1_; i++)
-      for (uint64_t p = U.yptr[i]; p < U.yptr[i + 1]; p++) vptr[U.ycol[p] + 1]++;
-    for (uint64_t j = 0; j < V.m; j++) vptr[j + 1] += vptr[j];
-    const uint64_t np = (uint64_t)vptr[V.m];
-    std::vector<uint32_t> vcol(np), u2v(U_.npos), v2u(np);
-    std::vector<int64_t> cur(vptr.begin(), vptr.end() - 1);
-    const uint64_t pb = U.yptr[u0_];
-    for (uint64_t i = u0_; i < u1_; i++)
-      for (uint64_t p = U.yptr[i]; p < U.yptr[i + 1]; p++) {
-        const uint64_t q = (uint64_t)cur[U.ycol[p]]++;
-        vcol[q] = (uint32_t)(i - u0_);
-        u2v[p - pb] = (uint32_t)q;
-        v2u[q] = (uint32_t)(p - pb);
+    auto vals = build_fields(V_, V, 0, V.m, V.Ds, B);
+    V_.npos = U_.npos;
+    if (!host_build_) {
+      // (U_.yptr / U_.ycol: this rank's user-major labels, build_user_side)
+      DevBuf<uint32_t> v2u, u2v;
+      B.transpose(U_.yptr, U_.ycol, U_.R, V.m, V_.yptr, V_.ycol, v2u, u2v);
+      if (comm_.active()) {  // the counts over ALL users (item side halves' CG steps, repl())
+        B.label_ptr(U, V.m, gvptr_);
+        gn1_ = (double)U.m;
       }
-    V_.npos = np;
-    if (comm_.active()) {  // the counts over ALL users (item side halves' CG steps, repl())
-      std::vector<int64_t> gptr(V.m + 1, 0);
-      for (uint64_t i = 0; i < U.m; i++)
-        for (uint64_t p = U.yptr[i]; p < U.yptr[i + 1]; p++) gptr[U.ycol[p] + 1]++;
-      for (uint64_t j = 0; j < V.m; j++) gptr[j + 1] += gptr[j];
-      gvptr_.upload(gptr);
-      gn1_ = (double)U.m;
+      build_segments_dev(V_, V_.yptr, V.m, vals, B);
+      V_.perm = std::move(v2u);
+      U_.perm = std::move(u2v);
+    } else {
+      std::vector<int64_t> vptr(V.m + 1, 0);
+      for (uint64_t i = u0_; i < u1_; i++)
+        for (uint64_t p = U.yptr[i]; p < U.yptr[i + 1]; p++) vptr[U.ycol[p] + 1]++;
+      for (uint64_t j = 0; j < V.m; j++) vptr[j + 1] += vptr[j];
+      const uint64_t np = (uint64_t)vptr[V.m];
+      std::vector<uint32_t> vcol(np), u2v(U_.npos), v2u(np);
+      std::vector<int64_t> cur(vptr.begin(), vptr.end() - 1);
+      const uint64_t pb = U.yptr[u0_];
+      for (uint64_t i = u0_; i < u1_; i++)
+        for (uint64_t p = U.yptr[i]; p < U.yptr[i + 1]; p++) {
+          const uint64_t q = (uint64_t)cur[U.ycol[p]]++;
+          vcol[q] = (uint32_t)(i - u0_);
+          u2v[p - pb] = (uint32_t)q;
+          v2u[q] = (uint32_t)(p - pb);
+        }
+      if (comm_.active()) {
+        std::vector<int64_t> gptr(V.m + 1, 0);
+        for (uint64_t i = 0; i < U.m; i++)
+          for (uint64_t p = U.yptr[i]; p < U.yptr[i + 1]; p++) gptr[U.ycol[p] + 1]++;
+        for (uint64_t j = 0; j < V.m; j++) gptr[j + 1] += gptr[j];
+        gvptr_.upload(gptr);
+        gn1_ = (double)U.m;
+      }
+      build_segments(V_, vptr, seg_len_, nsg());
+      V_.yptr.upload(vptr);
+      V_.ycol.upload(vcol);
+      V_.perm.upload(v2u);
+      U_.perm.upload(u2v);
     }
-    build_segments(V_, vptr, seg_len_, nsg());
-    V_.yptr.upload(vptr);
-    V_.ycol.upload(vcol);
-    V_.yt.alloc(std::max<uint64_t>(np, 1));
-    V_.perm.upload(v2u);
-    U_.perm.upload(u2v);
+    V_.yt.alloc(std::max<uint64_t>(V_.npos, 1));
     V_.bias.alloc(std::max<uint64_t>(V_.R, 1));
     V_.s.alloc(std::max<uint64_t>(V_.R, 1));
   }
 
-  void build_test(const HostData &Ut, const HostData &U) {
+  void build_test(const HostData &Ut, const HostData &U, dev::Builder &B) {
     const uint64_t t0 = Ut.m * (uint64_t)comm_.rank / (uint64_t)comm_.nranks;
     const uint64_t t1 = Ut.m * (uint64_t)(comm_.rank + 1) / (uint64_t)comm_.nranks;
     T_.R = t1 - t0;
     T_.R_glob = Ut.m;
     T_.row0 = t0;
     std::vector<uint64_t> Ds(U.Ds);  // test fields use the train Ds
-    build_fields(T_, Ut, t0, t1, Ds);
-    for (auto &F : T_.F) {
-      F->h_xptr.clear();
-      F->h_xidx.clear();
-      F->h_xval.clear();
+    build_fields(T_, Ut, t0, t1, Ds, B);
+    if (host_build_) {
+      for (auto &F : T_.F) {
+        F->h_xptr.clear();
+        F->h_xidx.clear();
+        F->h_xval.clear();
+      }
+      std::vector<int64_t> lptr(T_.R + 1);
+      const uint64_t lb = Ut.yptr[t0];
+      for (uint64_t i = 0; i <= T_.R; i++) lptr[i] = (int64_t)(Ut.yptr[t0 + i] - lb);
+      std::vector<uint32_t> lcol(Ut.yptr[t1] - lb);
+      for (uint64_t p = lb; p < Ut.yptr[t1]; p++)
+        lcol[p - lb] = (uint32_t)std::min<uint64_t>(Ut.ycol[p], 0xffffffffu);
+      T_.yptr.upload(lptr);
+      T_.ycol.upload(lcol);
+    } else {
+      B.labels(Ut, t0, t1, T_.yptr, T_.ycol);
     }
-    std::vector<int64_t> lptr(T_.R + 1);
-    const uint64_t lb = Ut.yptr[t0];
-    for (uint64_t i = 0; i <= T_.R; i++) lptr[i] = (int64_t)(Ut.yptr[t0 + i] - lb);
-    std::vector<uint32_t> lcol(Ut.yptr[t1] - lb);
-    for (uint64_t p = lb; p < Ut.yptr[t1]; p++)
-      lcol[p - lb] = (uint32_t)std::min<uint64_t>(Ut.ycol[p], 0xffffffffu);
-    T_.yptr.upload(lptr);
-    T_.ycol.upload(lcol);
     std::vector<uint8_t> cold(std::max<uint64_t>(T_.R, 1), 0);
     for (uint64_t i = 0; i < T_.R; i++) cold[i] = Ut.nnx[t0 + i] == 0;
     cold_.upload(cold);
   }
+
+  // fp64 values to the solver's precision on the device (the same rounding
+  // as the host's (real) cast)
+  void to_real_dev(const double *in, uint64_t n, DevBuf<real> &out) {
+    out.alloc(n, false);
+    if (!n) return;
+    if constexpr (std::is_same<real, double>::value) {
+      HIPCHK(hipMemcpyAsync(out.p, in, n * sizeof(double), hipMemcpyDeviceToDevice, stream_));
+    } else {
+      launch(k_to_real<real>, grid_for(n, BLOCK, 8192), BLOCK, 0, n, in, out.p);
+    }
+  }
+  void to_real_dev(const DevBuf<double> &in, DevBuf<real> &out) { to_real_dev(in.p, in.n, out); }
 
   std::vector<real> to_real(const std::vector<double> &v) {
     std::vector<real> o(v.size());
@@ -1683,12 +1919,9 @@ template <typename real> class Problem final : public ProblemBase {
   // chunk so that their G_c is stored as zero.  The chunks of a multi-chunk
   // column get consecutive partial slots (Job.slot) and their index in the
   // column (Job.flags).  The Gram buffers are allocated by col_grams.
-  void col_gram_chunks(DevField<real> &F, const std::vector<uint32_t> &xidx) {
+  void col_gram_chunks(DevField<real> &F, const std::vector<int64_t> &cptr) {
     const uint64_t ch = cgram32() ? (uint64_t)CGRAM32_ROWS
                                   : std::min<uint64_t>(cgram_chunk_, (uint64_t)cgram_rows((int)kp_, (int)sizeof(real)));
-    std::vector<uint64_t> cptr(F.D + 1, 0);
-    for (uint32_t c : xidx) cptr[c + 1]++;
-    for (uint64_t d = 0; d < F.D; d++) cptr[d + 1] += cptr[d];
     std::vector<Job> chunks, sums;
     uint64_t slots = 0;
     for (uint64_t d = 0; d < F.D; d++) {
@@ -2195,6 +2428,9 @@ template <typename real> class Problem final : public ProblemBase {
   uint64_t gram64_blocks_ = std::getenv("OCFFM_GRAM64_BLOCKS") ? std::strtoull(std::getenv("OCFFM_GRAM64_BLOCKS"), nullptr, 10) : 1024;
   uint64_t gram_blocks_ = std::getenv("OCFFM_GRAM_BLOCKS") ? std::strtoull(std::getenv("OCFFM_GRAM_BLOCKS"), nullptr, 10) : 512;
   bool no_owned_ = false;
+  // OCFFM_HOST_BUILD=1: the data layout built on the host (the checker of
+  // the device build, devbuild.h)
+  bool host_build_ = std::getenv("OCFFM_HOST_BUILD") != nullptr && std::atoi(std::getenv("OCFFM_HOST_BUILD")) != 0;
   bool owned_stale_ = false;  // owned tables differ across ranks until sync_owned()
   unsigned hs_blocks_ = 4096;  // grid cap of the cross Hessian-vector row pass
   unsigned feat_blocks_ = 1024;  // grid cap of the feature pass (grid-stride over jobs)
@@ -2278,8 +2514,7 @@ int ocffm_device_count(int *count) {
 int ocffm_data_read(const char *path, int has_label, const uint64_t *ds, uint32_t nds, ocffm_data **out) {
   return guarded([&] {
     auto d = std::make_unique<ocffm_data>();
-    Rows r = parse_rows(path, has_label != 0, ds, nds);
-    build(d->d, r);
+    build(d->d, parse_rows(path, has_label != 0, ds, nds));
     d->d.path = path;
     *out = d.release();
   });
@@ -2291,25 +2526,37 @@ int ocffm_data_from_rows(uint64_t m, const uint64_t *xptr, const uint32_t *fid, 
   return guarded([&] {
     Rows r;
     r.has_label = yptr != nullptr;
-    for (uint64_t i = 0; i < m; i++) {
-      for (uint64_t p = xptr[i]; p < xptr[i + 1]; p++) {
-        r.f = std::max<uint64_t>(r.f, (uint64_t)fid[p] + 1);
-        if (ds != nullptr && (fid[p] >= nds || ds[fid[p]] <= idx[p])) continue;
-        r.fid.push_back(fid[p]);
-        r.idx.push_back(idx[p]);
-        r.val.push_back(val[p]);
-      }
-      r.xptr.push_back(r.fid.size());
-      if (r.has_label) {
-        for (uint64_t p = yptr[i]; p < yptr[i + 1]; p++) {
-          r.ycol.push_back(ycol[p]);
-          r.n = std::max<uint64_t>(r.n, ycol[p] + 1);
+    const uint64_t nn = xptr[m] - xptr[0];
+    for (uint64_t p = xptr[0]; p < xptr[m]; p++) r.f = std::max<uint64_t>(r.f, (uint64_t)fid[p] + 1);
+    if (ds == nullptr) {  // every node kept: the arrays as given
+      r.xptr.resize(m + 1);
+      for (uint64_t i = 0; i <= m; i++) r.xptr[i] = xptr[i] - xptr[0];
+      r.fid.assign(fid + xptr[0], fid + xptr[m]);
+      r.idx.assign(idx + xptr[0], idx + xptr[m]);
+      r.val.assign(val + xptr[0], val + xptr[m]);
+    } else {
+      r.fid.reserve(nn);
+      r.idx.reserve(nn);
+      r.val.reserve(nn);
+      r.xptr.reserve(m + 1);
+      for (uint64_t i = 0; i < m; i++) {
+        for (uint64_t p = xptr[i]; p < xptr[i + 1]; p++) {
+          if (fid[p] >= nds || ds[fid[p]] <= idx[p]) continue;
+          r.fid.push_back(fid[p]);
+          r.idx.push_back(idx[p]);
+          r.val.push_back(val[p]);
         }
-        r.yptr.push_back(r.ycol.size());
+        r.xptr.push_back(r.fid.size());
       }
     }
+    if (r.has_label) {
+      r.yptr.resize(m + 1);
+      for (uint64_t i = 0; i <= m; i++) r.yptr[i] = yptr[i] - yptr[0];
+      r.ycol.assign(ycol + yptr[0], ycol + yptr[m]);
+      for (uint64_t j : r.ycol) r.n = std::max<uint64_t>(r.n, j + 1);
+    }
     auto d = std::make_unique<ocffm_data>();
-    build(d->d, r);
+    build(d->d, std::move(r));
     *out = d.release();
   });
 }
@@ -2323,9 +2570,7 @@ int ocffm_data_get_info(const ocffm_data *d, ocffm_data_info *o) {
     o->m = d->d.m;
     o->n = d->d.n;
     o->f = d->d.f;
-    uint64_t nx = 0;
-    for (auto &v : d->d.xidx) nx += v.size();
-    o->nnz_x = nx;
+    o->nnz_x = d->d.raw.fid.size();
     o->nnz_y = d->d.ycol.size();
   });
 }
@@ -2347,6 +2592,7 @@ int ocffm_data_get_field(const ocffm_data *d, uint32_t field, int64_t *xptr, uin
                          uint64_t *nnz) {
   return guarded([&] {
     if (field >= d->d.f) throw ocffm::Error(OCFFM_E_ARG, "no such field");
+    split_host(d->d);
     if (nnz) *nnz = d->d.xidx[field].size();
     if (xptr) std::copy(d->d.xptr[field].begin(), d->d.xptr[field].end(), xptr);
     if (xidx) std::copy(d->d.xidx[field].begin(), d->d.xidx[field].end(), xidx);
@@ -2548,6 +2794,17 @@ int ocffm_problem_reset_stats(ocffm_problem *prob) {
 }
 int ocffm_problem_alg_bytes(ocffm_problem *prob, double *bytes) { PROB_CALL(*bytes = prob->p->alg_bytes); }
 int ocffm_problem_sync(ocffm_problem *prob) { PROB_CALL(prob->p->sync()); }
+int ocffm_problem_layout_digest(ocffm_problem *prob, char *names, uint64_t *digests, int cap, int *count) {
+  return guarded([&] {
+    if (!prob || !prob->p || !count) throw Error(OCFFM_E_ARG, "null argument");
+    const auto d = prob->p->layout_digest();
+    *count = (int)d.size();
+    for (int i = 0; i < cap && i < (int)d.size(); i++) {
+      if (names) std::snprintf(names + 48 * (size_t)i, 48, "%s", d[i].first.c_str());
+      if (digests) digests[i] = d[i].second;
+    }
+  });
+}
 void ocffm_problem_destroy(ocffm_problem *prob) { delete prob; }
 
 }  // extern "C"

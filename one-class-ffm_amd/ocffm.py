@@ -68,7 +68,7 @@ EXPORTS = [
     "ocffm_problem_cg_log", "ocffm_problem_set_profiling", "ocffm_problem_set_profile_filter",
     "ocffm_problem_kernel_stats",
     "ocffm_problem_reset_stats", "ocffm_problem_alg_bytes", "ocffm_problem_sync",
-    "ocffm_problem_destroy",
+    "ocffm_problem_layout_digest", "ocffm_problem_destroy",
     "ocffm_sgd_param_default", "ocffm_sgd_create", "ocffm_sgd_create_dist", "ocffm_sgd_create_dist_host", "ocffm_sgd_epoch",
     "ocffm_sgd_average", "ocffm_sgd_phi", "ocffm_sgd_get", "ocffm_sgd_set_w", "ocffm_sgd_get_info",
     "ocffm_sgd_sync", "ocffm_sgd_destroy",
@@ -121,6 +121,7 @@ def lib():
     L.ocffm_problem_set_profile_filter.argtypes = [vp, C.c_char_p]
     L.ocffm_problem_kernel_stats.argtypes = [vp, C.POINTER(_KStat), i32, C.POINTER(C.c_int)]
     L.ocffm_problem_alg_bytes.argtypes = [vp, C.POINTER(dbl)]
+    L.ocffm_problem_layout_digest.argtypes = [vp, vp, vp, i32, C.POINTER(C.c_int)]
     L.ocffm_problem_destroy.argtypes = [vp]
     L.ocffm_problem_destroy.restype = None
     L.ocffm_sgd_param_default.argtypes = [vp]
@@ -484,6 +485,16 @@ class ImpProblem:
 
     def sync(self) -> None:
         _check(lib().ocffm_problem_sync(self.h))
+
+    def layout_digest(self) -> dict:
+        """{array name: FNV-1a digest} of the device data layout (ocffm.h)."""
+        n = C.c_int(0)
+        _check(lib().ocffm_problem_layout_digest(self.h, None, None, 0, C.byref(n)))
+        names = C.create_string_buffer(48 * max(1, n.value))
+        dig = (C.c_uint64 * max(1, n.value))()
+        _check(lib().ocffm_problem_layout_digest(self.h, names, dig, n.value, C.byref(n)))
+        raw = names.raw
+        return {raw[48 * i:48 * (i + 1)].split(b"\0", 1)[0].decode(): int(dig[i]) for i in range(n.value)}
 
 
 def srand(seed: int = 1) -> None:

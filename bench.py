@@ -73,10 +73,15 @@ def run_newton(ds, prec, steps, warmup, k=32, self_side=True, world=1, rank=0, l
     """Warm-up (finds the dominant kernel family), K timed epochs (barrier +
     device sync on both sides, max over ranks), then the same K epochs again
     with the dominant family's dispatches carrying HIP events (roofline)."""
+    ts = time.perf_counter()
     g = ocffm.problem_from_dataset(ds, precision=prec, with_test=False, device=local, rank=rank, nranks=world,
                                    comm=comm, allreduce=allreduce, k=k, self_side=self_side)
+    t_create = time.perf_counter() - ts
+    ts = time.perf_counter()
     ocffm.srand(1)
     g.init()
+    g.sync()
+    t_init = time.perf_counter() - ts
 
     def barrier():
         g.sync()
@@ -147,7 +152,8 @@ def run_newton(ds, prec, steps, warmup, k=32, self_side=True, world=1, rank=0, l
             roof["traffic"] = None if t is None else round(t["bytes_per_launch"])
         except Exception:
             pass
-    return dict(dt=dt, roof=roof, cg_per_epoch=round(cg.sum() / max(1, steps), 1))
+    return dict(dt=dt, roof=roof, cg_per_epoch=round(cg.sum() / max(1, steps), 1),
+                setup_s={"create": round(t_create, 3), "init": round(t_init, 3)})
 
 
 def main():
@@ -249,7 +255,8 @@ def cfg5_mode(args):
                            "rows_per_gpu": CFG5_ROWS, "items": int(ds.item.m), "positives": ds.n_positives,
                            "user_fields": 39, "item_fields": 1, "features_per_field": 250000, "k": 64,
                            "self_side": False, "cg_iters_per_epoch": r["cg_per_epoch"],
-                           "p_cache_GB": round(39 * CFG5_ROWS * 64 * 4 / 1e9, 1), "datagen_s": round(gen, 1)},
+                           "p_cache_GB": round(39 * CFG5_ROWS * 64 * 4 / 1e9, 1), "datagen_s": round(gen, 1),
+                           "setup_s": r["setup_s"]},
                 "roofline": r["roof"]}
     except Exception as e:  # never blocks the headline number
         return {"value": None, "error": str(e)}

@@ -140,6 +140,14 @@ class Builder {
   Scratch scr_;
 };
 
+// init_mat (ffm.cpp:71-78) on the device: table (rows x cols doubles in
+// row-major draw order) into out (row stride kp, padding untouched), the
+// values init_table draws on the host bit for bit (minstd_rand0 jump-ahead
+// per lane; generate_canonical<double, 53> and uniform_real_distribution
+// with the two FMA contractions g++ -mfma makes in host_data.cpp).
+template <typename real>
+void draw_table(hipStream_t s, real *out, uint64_t rows, uint32_t cols, uint32_t kp, const TableDraw &t);
+
 // The column-tau weight of a one-node field, sum of x^2 over a column's
 // entries v[0, n) (in row order), in the order k_xsq adds them: 256 strided
 // partials p[t] = v[t]^2 + v[t+256]^2 + ..., then p[t] += p[t + o] for

@@ -324,7 +324,60 @@ __global__ void __launch_bounds__(TB) k_scan_apply(uint64_t n, const int64_t *__
   }
 }
 
+// --------------------------------------------------------------- init_mat
+// minstd_rand0: x' = 16807 x mod (2^31 - 1), reduced without a division
+__device__ __forceinline__ uint64_t lcg_mul(uint64_t x, uint64_t a) {
+  const uint64_t p = x * a;  // < 2^62
+  const uint64_t r = (p & 0x7fffffffull) + (p >> 31);
+  return r >= 0x7fffffffull ? r - 0x7fffffffull : r;
+}
+__device__ __forceinline__ uint64_t lcg_pow(uint64_t e) {
+  uint64_t r = 1, a = 16807;
+  for (; e; e >>= 1, a = lcg_mul(a, a))
+    if (e & 1) r = lcg_mul(r, a);
+  return r;
+}
+
+// A wave draws DRAW_RUN consecutive values per lane, interleaved: lane l
+// takes values base + l + 64 j (coalesced stores), so its engine state jumps
+// 128 steps (A^128) between its values.  Value i consumes engine outputs
+// 2i + 1 and 2i + 2 of the table's stream.
+constexpr int DRAW_RUN = 64;
+template <typename real>
+__global__ void __launch_bounds__(TB) k_draw(uint64_t n, uint32_t cols, uint32_t kp, uint64_t x0, double a,
+                                             double width, double r2, uint64_t a128, real *__restrict__ out) {
+  const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / 64, lane = threadIdx.x % 64;
+  const uint64_t base = wave * 64 * DRAW_RUN;
+  if (base >= n) return;
+  uint64_t x = lcg_mul(x0, lcg_pow(2 * (base + lane)));  // state before value base + lane
+  for (int j = 0; j < DRAW_RUN; j++) {
+    const uint64_t i = base + lane + 64 * (uint64_t)j;
+    if (i >= n) break;
+    const uint64_t u1 = lcg_mul(x, 16807), u2 = lcg_mul(u1, 16807);
+    const double sum = __fma_rn((double)(u2 - 1), 2147483646.0, (double)(u1 - 1));
+    double c = __ddiv_rn(sum, r2);
+    if (c >= 1.0) c = 0x1.fffffffffffffp-1;  // nextafter(1, 0)
+    const double v = __fma_rn(c, width, a);
+    out[(i / cols) * kp + (i % cols)] = (real)v;
+    x = lcg_mul(x, a128);
+  }
+}
+
 }  // namespace
+
+template <typename real>
+void draw_table(hipStream_t s, real *out, uint64_t rows, uint32_t cols, uint32_t kp, const TableDraw &t) {
+  const uint64_t n = rows * cols;
+  if (!n) return;
+  uint64_t a128 = 1;
+  for (int q = 0; q < 128; q++) a128 = a128 * 16807 % 0x7fffffffull;
+  const uint64_t waves = (n + 64 * DRAW_RUN - 1) / (64 * DRAW_RUN);
+  const uint64_t blocks = (waves * 64 + TB - 1) / TB;
+  hipLaunchKernelGGL(k_draw<real>, (unsigned)blocks, TB, 0, s, n, cols, kp, t.x0, t.a, t.width, t.r2, a128, out);
+  HIPCHK(hipGetLastError());
+}
+template void draw_table<float>(hipStream_t, float *, uint64_t, uint32_t, uint32_t, const TableDraw &);
+template void draw_table<double>(hipStream_t, double *, uint64_t, uint32_t, uint32_t, const TableDraw &);
 
 // ---------------------------------------------------------------- host side
 void Builder::incl_scan(const int64_t *in, int64_t *out, uint64_t n) {

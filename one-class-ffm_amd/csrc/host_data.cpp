@@ -367,6 +367,20 @@ static uint64_t powmod(uint64_t a, uint64_t e, uint64_t m) {
   return r;
 }
 
+TableDraw table_draw(uint32_t cols) {
+  using E = std::minstd_rand0;
+  const uint64_t seed = (uint64_t)(unsigned)std::rand();
+  const double b = 0.1 * qrsqrt((double)cols);
+  TableDraw t;
+  t.x0 = seed % E::modulus;
+  if (t.x0 == 0) t.x0 = 1;
+  t.a = -b;
+  t.width = b - t.a;  // uniform_real_distribution: a + (b - a) * canonical
+  const long double r = (long double)E::max() - (long double)E::min() + 1.0L;
+  t.r2 = (double)((long double)(double)r * r);  // generate_canonical's tmp after two rounds
+  return t;
+}
+
 void init_table(double *out, uint64_t rows, uint32_t cols) {
   using E = std::minstd_rand0;
   const uint64_t seed = (uint64_t)(unsigned)std::rand();

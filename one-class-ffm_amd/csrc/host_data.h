@@ -59,4 +59,14 @@ void trans_y(HostData &V, const HostData &U);
 // Compiled with FMA contraction so the stream matches a -march=native build.
 void init_table(double *out, uint64_t rows, uint32_t cols);
 
+// The same draw's parameters for the device (devbuild.h draw_table): one
+// rand() call (the engine seed, reduced as linear_congruential_engine::seed
+// does), the distribution's a = -b and b - a, and the divisor of
+// generate_canonical<double, 53> (r^2 rounded to double, r = 2^31 - 2).
+struct TableDraw {
+  uint64_t x0;
+  double a, width, r2;
+};
+TableDraw table_draw(uint32_t cols);
+
 }  // namespace ocffm

@@ -1355,7 +1355,13 @@ template <typename real> class Problem final : public ProblemBase {
     return o;
   }
 
+  // init_mat (ffm.cpp:71-78): drawn on the device (devbuild.h draw_table;
+  // OCFFM_HOST_INIT=1: on the host and uploaded), the same values either way.
   void upload_table(DevBuf<real> &t, uint64_t D) {
+    if (!host_init_) {
+      dev::draw_table<real>(stream_, t.p, D, k_, kp_, table_draw(k_));
+      return;
+    }
     std::vector<double> host(D * k_);
     init_table(host.data(), D, k_);
     std::vector<real> pad(D * kp_, (real)0);
@@ -2431,6 +2437,7 @@ template <typename real> class Problem final : public ProblemBase {
   // OCFFM_HOST_BUILD=1: the data layout built on the host (the checker of
   // the device build, devbuild.h)
   bool host_build_ = std::getenv("OCFFM_HOST_BUILD") != nullptr && std::atoi(std::getenv("OCFFM_HOST_BUILD")) != 0;
+  bool host_init_ = std::getenv("OCFFM_HOST_INIT") != nullptr && std::atoi(std::getenv("OCFFM_HOST_INIT")) != 0;
   bool owned_stale_ = false;  // owned tables differ across ranks until sync_owned()
   unsigned hs_blocks_ = 4096;  // grid cap of the cross Hessian-vector row pass
   unsigned feat_blocks_ = 1024;  // grid cap of the feature pass (grid-stride over jobs)

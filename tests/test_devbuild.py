@@ -127,3 +127,25 @@ def test_device_build_trains_like_host_build(monkeypatch):
         g.close()
     for a, b in zip(out[0], out[1]):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("precision", [ocffm.FP32, ocffm.FP64])
+@pytest.mark.parametrize("k", [1, 5, 32, 37, 64, 100])
+def test_device_draw_equals_host_draw(monkeypatch, precision, k):
+    """init_mat (ffm.cpp:71-78) drawn on the device (minstd_rand0 jump-ahead,
+    generate_canonical, uniform_real_distribution) equals the host draw of
+    init_table bit for bit (and P, Q = X W, X H computed from them)."""
+    ds = synth.tiny(seed=3, m=300)
+    tabs = []
+    for host in (False, True):
+        if host:
+            monkeypatch.setenv("OCFFM_HOST_INIT", "1")
+        else:
+            monkeypatch.delenv("OCFFM_HOST_INIT", raising=False)
+        g = ocffm.problem_from_dataset(ds, precision=precision, with_test=False, k=k)
+        ocffm.srand(1)
+        g.init()
+        tabs.append([g.get(w, b).copy() for b in range(g.n_blocks()) for w in "WHPQ"])
+        g.close()
+    for a, b in zip(tabs[0], tabs[1]):
+        np.testing.assert_array_equal(a, b)

@@ -2047,17 +2047,20 @@ __global__ __launch_bounds__(BLOCK) void k_gram_mfma32(uint64_t Rp, const float 
 // Cross-half aggregates at KP = 64, fp32, on MFMA (gd_cross / cg,
 // ffm.cpp:660-670, 767-771): M_c = A_c^T B for every partner-side table A_c
 // (k x k, c < C), oQ = sum_i B_i, bQ = sum_i wv_i B_i and sum wv, over the
-// rows of block x's chunk.  Each wave owns GW tables (4 x 16 accumulator
-// registers per table: the 2 x 2 tiles of 32 x 32) and walks every row of
-// the chunk: v_mfma_f32_32x32x2f32 takes a row pair as the K dimension,
-// lane l supplying A_c[row 2u + l/32][32 mt + l%32] and B[row][32 nt + l%32]
-// (dword loads: a half-wave reads one 128-B half-row), two register sets so
-// that the next round's loads are in flight.  The block's four waves read
-// the same B rows (L1 hits) for four table groups.  Block b takes table
-// group b % ng and row chunk b / ng, so the blocks of one chunk are
-// dispatched together and share its B rows in the Infinity Cache.
-// Partials: part[chunk][c * 4096 + m * 64 + n] and, from group 0, wave 0,
-// the sums at [C * 4096 ..) (k_reduce_parts, fixed order).
+// rows of block x's chunk.  Wave slot c < C owns table c (4 x 16 accumulator
+// registers: the 2 x 2 tiles of 32 x 32) and walks every row of the chunk:
+// v_mfma_f32_32x32x2f32 takes a row pair as the K dimension, lane l
+// supplying A_c[row 2u + l/32][32 mt + l%32] and B[row][32 nt + l%32] (dword
+// loads: a half-wave reads one 128-B half-row), two register sets so that
+// the next round's loads are in flight.  Wave slot C computes the sums on
+// the matrix cores too, as S^T B with S_i = [1, wv_i, 0, ...] (rows 0 and 1
+// of its first row tile), plus sum wv: summing on the VALU in one of the
+// table waves had slowed the whole launch by 14 % (f32 VALU and f32 MFMA
+// share the SIMD's f32 rate; tools/mb/mb_gram64.hip).  The block's four
+// waves read the same B rows (L1 hits).  Block b takes slot group b % ng and
+// row chunk b / ng, so the blocks of one chunk are dispatched together and
+// share its B rows in the Infinity Cache.  Partials: part[chunk][c * 4096 +
+// m * 64 + n] and the sums at [C * 4096 ..) (k_reduce_parts, fixed order).
 constexpr int GW64 = 1;  // tables per wave of k_gram_mfma64 (64 accumulators each)
 static __global__ __launch_bounds__(BLOCK, 3) void k_gram_mfma64(uint64_t Rp, int C, const float *const *__restrict__ A,
                                                        const float *__restrict__ B, const float *__restrict__ wv,
@@ -2068,60 +2071,72 @@ static __global__ __launch_bounds__(BLOCK, 3) void k_gram_mfma64(uint64_t Rp, in
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int e = lane & 31, hf = lane >> 5;
   const unsigned grp = blockIdx.x % ngroups, chunk = blockIdx.x / ngroups;
-  const int c0 = (int)(grp * (BLOCK / 64) + w) * GW64;
-  const int nc = C - c0 < 0 ? 0 : (C - c0 < GW64 ? C - c0 : GW64);  // wave-uniform
-  const bool sums = grp == 0 && w == 0;
-  if (nc == 0) return;  // no barrier below
-  f16x acc[GW64][4];
+  const int c0 = (int)(grp * (BLOCK / 64) + w);
+  if (c0 > C) return;  // no barrier below
+  f16x acc[4];
 #pragma unroll
-  for (int c = 0; c < GW64; c++)
+  for (int t = 0; t < 4; t++)
 #pragma unroll
-    for (int t = 0; t < 4; t++)
-#pragma unroll
-      for (int r = 0; r < 16; r++) acc[c][t][r] = 0.0f;
-  BufView ab[GW64];
-#pragma unroll
-  for (int c = 0; c < GW64; c++) ab[c] = buf_view(c < nc ? A[c0 + c] : nullptr, c < nc ? Rp * 256 : 0);
-  const BufView bb = buf_view(B, Rp * 256), wb = buf_view(wv, wv ? Rp * 4 : 0);
+    for (int r = 0; r < 16; r++) acc[t][r] = 0.0f;
+  const BufView bb = buf_view(B, Rp * 256);
   const uint64_t r0 = (uint64_t)chunk * rows_per_block;
   const uint64_t r1 = r0 + rows_per_block < Rp ? r0 + rows_per_block : Rp;
-  float cs[2] = {0, 0}, ws[2] = {0, 0}, wt = 0;
-  float bv[2][U][2], av[2][U][GW64][2], wvv[2][U];
+  float *out = part + (size_t)chunk * nout;
+  if (c0 == C) {  // the sums slot: S^T B, S_i = [1, wv_i, 0, ...]; rows past r1 meet B = 0
+    const BufView wb = buf_view(wv, wv ? Rp * 4 : 0);
+    float wt = 0;
+    for (uint64_t j0 = r0; j0 < r1; j0 += 2 * U) {
+      float bv[U][2], sv[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t jj = j0 + 2 * u + hf;
+        const bool ok = jj < r1;
+        const uint32_t off = ok ? (uint32_t)(jj * 256 + e * 4) : 0xffffff00u;
+#pragma unroll
+        for (int h = 0; h < 2; h++) bv[u][h] = bld1<float>(bb, off + h * 128);
+        const float wvi = bld1<float>(wb, ok ? (uint32_t)(jj * 4) : 0xffffff00u);
+        sv[u] = e == 0 ? 1.0f : (e == 1 ? wvi : 0.0f);
+        if (e == 0) wt += wvi;
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++) acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(sv[u], bv[u][nt], acc[nt], 0, 0, 0);
+    }
+    // D row m = 0 (lanes hf = 0, register 0) is sum B, row 1 (register 1) sum wv B
+    wt += __shfl_xor(wt, 32, 64);  // lanes 0 and 32 hold the even / odd rows' sums
+    if (hf == 0) {
+#pragma unroll
+      for (int nt = 0; nt < 2; nt++) {
+        out[(size_t)C * 4096 + nt * 32 + e] = acc[nt][0];
+        out[(size_t)C * 4096 + 64 + nt * 32 + e] = acc[nt][1];
+      }
+      if (e == 0) out[(size_t)C * 4096 + 128] = wt;
+    }
+    return;
+  }
+  const BufView ab = buf_view(A[c0], Rp * 256);
+  float bv[2][U][2], av[2][U][2];
   auto load = [&](int sb, uint64_t j0) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint64_t jj = j0 + 2 * u + hf;
-      const bool ok = jj < r1;
-      const uint32_t off = ok ? (uint32_t)(jj * 256 + e * 4) : 0xffffff00u;
+      const uint32_t off = jj < r1 ? (uint32_t)(jj * 256 + e * 4) : 0xffffff00u;
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         bv[sb][u][h] = bld1<float>(bb, off + h * 128);
-#pragma unroll
-        for (int c = 0; c < GW64; c++) av[sb][u][c][h] = bld1<float>(ab[c], off + h * 128);
+        av[sb][u][h] = bld1<float>(ab, off + h * 128);
       }
-      wvv[sb][u] = bld1<float>(wb, ok ? (uint32_t)(jj * 4) : 0xffffff00u);
     }
   };
   auto step = [&](int sb) {
 #pragma unroll
-    for (int u = 0; u < U; u++) {
+    for (int u = 0; u < U; u++)
 #pragma unroll
-      for (int c = 0; c < GW64; c++)
+      for (int mt = 0; mt < 2; mt++)
 #pragma unroll
-        for (int mt = 0; mt < 2; mt++)
-#pragma unroll
-          for (int nt = 0; nt < 2; nt++)
-            acc[c][mt * 2 + nt] =
-                __builtin_amdgcn_mfma_f32_32x32x2f32(av[sb][u][c][mt], bv[sb][u][nt], acc[c][mt * 2 + nt], 0, 0, 0);
-      if (sums) {
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-          cs[h] += bv[sb][u][h];
-          ws[h] += wvv[sb][u] * bv[sb][u][h];
-        }
-        if (e == 0) wt += wvv[sb][u];
-      }
-    }
+        for (int nt = 0; nt < 2; nt++)
+          acc[mt * 2 + nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[sb][u][mt], bv[sb][u][nt], acc[mt * 2 + nt], 0, 0, 0);
   };
   // rows past r1 load zeros (buffer range check), so a trailing round is harmless
   for (uint64_t j0 = r0; j0 < r1; j0 += 4 * U) {
@@ -2130,34 +2145,13 @@ static __global__ __launch_bounds__(BLOCK, 3) void k_gram_mfma64(uint64_t Rp, in
     step(0);
     step(1);
   }
-  float *out = part + (size_t)chunk * nout;
 #pragma unroll
-  for (int c = 0; c < GW64; c++) {
-    if (c >= nc) break;
+  for (int t = 0; t < 4; t++)
 #pragma unroll
-    for (int t = 0; t < 4; t++)
-#pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const int m = (t >> 1) * 32 + 8 * (r >> 2) + 4 * hf + (r & 3), n = (t & 1) * 32 + e;
-        out[(size_t)(c0 + c) * 4096 + m * 64 + n] = acc[c][t][r];
-      }
-  }
-  if (sums) {  // the two half-waves hold the even / odd rows of the same column
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      cs[h] += __shfl_xor(cs[h], 32, 64);
-      ws[h] += __shfl_xor(ws[h], 32, 64);
+    for (int r = 0; r < 16; r++) {
+      const int m = (t >> 1) * 32 + 8 * (r >> 2) + 4 * hf + (r & 3), n = (t & 1) * 32 + e;
+      out[(size_t)c0 * 4096 + m * 64 + n] = acc[t][r];
     }
-    wt += __shfl_xor(wt, 32, 64);
-    if (hf == 0) {
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        out[(size_t)C * 4096 + h * 32 + e] = cs[h];
-        out[(size_t)C * 4096 + 64 + h * 32 + e] = ws[h];
-      }
-      if (e == 0) out[(size_t)C * 4096 + 128] = wt;
-    }
-  }
 }
 
 // o in [0, cnt): t = sum_b part[b][off + o]; o < split -> out_real[o] = t,

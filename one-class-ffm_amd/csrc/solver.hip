@@ -1554,7 +1554,7 @@ template <typename real> class Problem final : public ProblemBase {
   void gram64(uint64_t Rp, int L, const real *const *A, const real *B, const real *wv, real *M) {
     if (!M || !B) throw Error(OCFFM_E_STATE, "gram64: Grams and partner table required");
     constexpr int TPB = (BLOCK / 64) * GW64;  // tables per block
-    const unsigned gy = (unsigned)((L + TPB - 1) / TPB);
+    const unsigned gy = (unsigned)((L + 1 + TPB - 1) / TPB);  // L table slots + the sums slot
     const uint64_t nout = (uint64_t)L * 4096 + 129;
     uint64_t nbx = std::max<uint64_t>(1, std::min<uint64_t>((Rp + 63) / 64, std::max<uint64_t>(1, gram64_blocks_ / gy)));
     const uint64_t rpb = ((Rp + nbx - 1) / nbx + 15) / 16 * 16;  // whole rounds of row pairs

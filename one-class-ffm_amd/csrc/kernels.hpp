@@ -730,7 +730,9 @@ template <int KP> struct RowsT {
   static constexpr int NT = KP / 32;  // 32-column output tiles
   static constexpr int KH = KP / 2;   // K steps per table (two K values each)
   static constexpr int TW = 2;        // 32-row tiles per wave
-  static constexpr int TG = KP == 64 ? 8 : 32;  // tables per LDS stage (128 KB)
+  // tables per LDS stage: KP = 64 two (32 KB; 8 tables / 128 KB measured 8 % slower,
+  // tools/mb/mb_rowsT.hip), KP = 32 all 32 of a stage (128 KB)
+  static constexpr int TG = KP == 64 ? 2 : 32;
   static constexpr int ROWS = (TBLOCK / 64) * TW * 32;  // rows per block pass
 };
 template <int KP>

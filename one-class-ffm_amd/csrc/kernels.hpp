@@ -425,20 +425,30 @@ __device__ __forceinline__ bool last_block(const double (&v)[NV], double *part, 
 #pragma unroll
       for (int k = 0; k < NV; k++) x[k] += y[u][k];
   }
+  if (nextra) {  // the extra slots: all rounds' loads in flight, then added in
+                 // a fixed order (thread, round) before the one block tree.
+                 // (One dependent round per BLOCK slots had cost feature passes
+                 // with ~1,000 heavy-column slots ~3 us each.)
+    const BufView ev = buf_view(extra, (uint64_t)nextra * NV * sizeof(double));
+    constexpr int ER = 8;
+    for (uint32_t q0 = 0; q0 < nextra; q0 += ER * BLOCK) {
+      double z[ER][NV];
+#pragma unroll
+      for (int u = 0; u < ER; u++)
+#pragma unroll
+        for (int k = 0; k < NV; k++) {
+          const uint32_t q = q0 + u * BLOCK + threadIdx.x;
+          z[u][k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                   ev.r, q < nextra ? (q * NV + k) * 8u : ev.oob, 0, 16));
+        }
+#pragma unroll
+      for (int u = 0; u < ER; u++)
+#pragma unroll
+        for (int k = 0; k < NV; k++) x[k] += z[u][k];
+    }
+  }
 #pragma unroll
   for (int k = 0; k < NV; k++) tot[k] = block_sum(x[k]);
-  if (nextra) {  // the extra slots, thread-strided then the fixed block tree
-    const BufView ev = buf_view(extra, (uint64_t)nextra * NV * sizeof(double));
-    double y[NV];
-#pragma unroll
-    for (int k = 0; k < NV; k++) y[k] = 0;
-    for (uint32_t q = threadIdx.x; q < nextra; q += BLOCK)
-#pragma unroll
-      for (int k = 0; k < NV; k++)
-        y[k] += __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ev.r, (q * NV + k) * 8u, 0, 16));
-#pragma unroll
-    for (int k = 0; k < NV; k++) tot[k] += block_sum(y[k]);
-  }
   if (threadIdx.x == 0) __hip_atomic_store(tick, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
 }

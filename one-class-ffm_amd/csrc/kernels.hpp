@@ -1503,6 +1503,7 @@ __global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__res
   const uint64_t wave = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
   const int sg = lane / G::LPR, li = lane % G::LPR;
   double dsum[3] = {0, 0, 0};
+  bool hd_stored = false;  // this wave stored a heavy column's dot-product slot
   const uint64_t nwaves = ((uint64_t)gridDim.x * BLOCK) >> 6;
   Job nxt = wave < nwave ? jobs[wave * G::NSG + sg] : Job{JOB_NONE, 1u, 0u, 0u, 0, 0};
   for (uint64_t w = wave; w < nwave; w += nwaves) {
@@ -1599,11 +1600,14 @@ __global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__res
 #pragma unroll
           for (int k = 0; k < 3; k++)
             __hip_atomic_store(f.hdots + (size_t)hslot * 3 + k, cd[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        hd_stored = true;
       } else col_finalize<real, KP, (MODE == 2 ? 0 : MODE), TAU>(f, jb.col, s, alpha, beta, upd, li, dsum, ops, Qs);
     }
   }
-  // the slot stores above are drained before this block's ticket (last_block)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // a wave's dot-product slot stores are drained before this block's ticket
+  // (last_block); waves that stored none do not wait for their vector stores
+  // (wave jobs are wave-uniform, so is the flag)
+  if (__any(hd_stored)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (MODE != 2) fin_blocks<real, (MODE == 2 ? 0 : MODE)>(f, dsum);
 }
 

@@ -5,19 +5,26 @@ one training epoch (ImpProblem::one_epoch, ffm.cpp:852-870) over the
 synthetic kkbox-shaped rows (SURVEY §8d, configs[2]); instances = training
 rows.  Inputs are resident in HBM before the timed region.
 
-Multi-GPU (torchrun, one process per GPU): weak scaling — each rank owns a
+Multi-GPU (one process per GPU): weak scaling — each rank owns a
 kkbox-shaped user shard of 30,755 rows (the items are shared), the gradient
 and Hessian-vector partial sums are all-reduced with RCCL inside the
 library; torch.distributed (gloo) is only the control plane (comm-id
-broadcast, barrier, max-over-ranks timing).
+broadcast, barrier, max-over-ranks timing).  Launched either by torchrun
+(RANK / WORLD_SIZE in the environment) or as `python bench.py --gpus N`:
+without WORLD_SIZE and with N > 1 this process starts N child ranks of
+itself (fresh interpreters, nothing here has touched the GPU yet) and exits
+with their status; rank 0 prints the line.
 
 The JSON line also carries:
-  roofline     — the dominant kernel family: algorithmic bytes per launch
-                  / its HIP-event-measured average
-                 duration on the solver stream, over a second pass of the
-                 same K epochs right after the (uninstrumented) timed region.
+  roofline     — the dominant kernel family (the most kernel time over a
+                 second pass of the same K epochs right after the
+                 uninstrumented timed region, every dispatch carrying HIP
+                 events on the solver stream): algorithmic bytes per launch
+                  / its average event-measured duration.
   cpu_baseline — the CPU oracle (clean-room OpenMP port of the reference,
-                 fp64) timed on this host on a bounded sample, rank 0, N=1.
+                 fp64) timed on this host on a bounded sample, rank 0, N=1:
+                 the same epoch window as the GPU's first timed epochs (the
+                 oracle starts from the GPU's tables after the warm-up).
   modes        — (N=1) the same kkbox epochs in fp64 (the reference's own
                  arithmetic, the parity mode); the config-5 shard (BASELINE
                  configs[4] restated, SURVEY §8d: 2 M rows, 39+1 fields,
@@ -30,6 +37,9 @@ import argparse
 import glob
 import json
 import os
+import resource
+import socket
+import subprocess
 import sys
 import time
 
@@ -48,7 +58,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32), dense
 RIDGE_FLOP_PER_B = MFMA_F32_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)
 ROWS_PER_GPU = 30755
-CFG5_ROWS = 2_000_000
+CFG5_ROWS = 12_500_000  # BASELINE configs[4]: 100 M rows over 8 GPUs
 
 
 def parse():
@@ -64,15 +74,37 @@ def parse():
                     help="N=1: also time the SGD/AdaGrad mode (tools/bench_sgd.py) into 'modes'")
     ap.add_argument("--modes", choices=["auto", "off"], default="auto",
                     help="N=1: also time the fp64 parity mode and the config-5 shard into 'modes'")
-    ap.add_argument("--cfg5-steps", type=int, default=3, help="timed epochs of the config-5 mode (<= --steps)")
+    ap.add_argument("--cfg5-steps", type=int, default=2, help="timed epochs of the config-5 mode (<= --steps)")
+    ap.add_argument("--cfg5-rows", type=int, default=CFG5_ROWS, help="rows of the config-5 shard")
     return ap.parse_args()
 
 
+def spawn_ranks(n):
+    """`bench.py --gpus N` outside torchrun: N fresh child processes of this
+    script, one per GPU (LOCAL_RANK = rank), rendezvous on 127.0.0.1.  The
+    parent has not touched the GPU; it waits and returns the worst status."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OCFFM_BENCH_LAUNCHER="spawn")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        p.wait()
+        rc = rc or p.returncode
+    return rc
+
+
 def run_newton(ds, prec, steps, warmup, k=32, self_side=True, world=1, rank=0, local=0, comm=None, allreduce=None,
-               pmc_tag=""):
-    """Warm-up (finds the dominant kernel family), K timed epochs (barrier +
-    device sync on both sides, max over ranks), then the same K epochs again
-    with the dominant family's dispatches carrying HIP events (roofline)."""
+               pmc_tag="", snapshot=None):
+    """W warm-up epochs, K timed epochs (barrier + device sync on both sides,
+    max over ranks, no instrumentation), then the same K epochs again with
+    every dispatch carrying HIP events: the family with the most kernel
+    time over that pass is the dominant one, its average launch the
+    roofline's.  snapshot(g): called after the warm-up (CPU baseline)."""
     ts = time.perf_counter()
     g = ocffm.problem_from_dataset(ds, precision=prec, with_test=False, device=local, rank=rank, nranks=world,
                                    comm=comm, allreduce=allreduce, k=k, self_side=self_side)
@@ -88,14 +120,11 @@ def run_newton(ds, prec, steps, warmup, k=32, self_side=True, world=1, rank=0, l
         if world > 1:
             dist.barrier()
 
-    g.set_profiling(True)
     for _ in range(max(1, warmup)):
         g.one_epoch()
-    ks = g.kernel_stats()
-    dominant = max(((kk, v) for kk, v in ks.items() if not kk.startswith("half(")),
-                   key=lambda kv: kv[1]["total_ms"])[0]
-    g.reset_stats()
-    g.set_profiling(False)
+    if snapshot is not None:
+        snapshot(g)
+    cg0 = g.cg_log().size
 
     # timed region: K epochs, no instrumentation (event-carrying dispatches
     # cost ~7 us each and would perturb the wall clock)
@@ -109,12 +138,11 @@ def run_newton(ds, prec, steps, warmup, k=32, self_side=True, world=1, rank=0, l
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    cg = g.cg_log()
+    cg = g.cg_log()[cg0:]
     alg = g.alg_bytes()
-    # kernel-timing pass: the same K epochs again, the dominant family's
-    # dispatches carrying start/stop HIP events on the solver stream
+    # kernel-timing pass: the same K epochs again, every dispatch carrying
+    # start/stop HIP events on the solver stream
     g.reset_stats()
-    g.set_profile_filter(dominant)
     g.set_profiling(True)
     for _ in range(steps):
         g.one_epoch()
@@ -122,7 +150,9 @@ def run_newton(ds, prec, steps, warmup, k=32, self_side=True, world=1, rank=0, l
     ks = g.kernel_stats()
     g.close()
 
-    d = ks.get(dominant, dict(launches=0, total_ms=0.0, alg_bytes=0.0, alg_flops=0.0))
+    fams = {kk: v for kk, v in ks.items() if not kk.startswith("half(") and not kk.endswith(".noop")}
+    dominant = max(fams.items(), key=lambda kv: kv[1]["total_ms"])[0]
+    d = ks[dominant]
     avg_ms = d["total_ms"] / max(1, d["launches"])
     bytes_per_launch = d["alg_bytes"] / max(1, d["launches"])
     flops_per_launch = d.get("alg_flops", 0.0) / max(1, d["launches"])
@@ -136,9 +166,12 @@ def run_newton(ds, prec, steps, warmup, k=32, self_side=True, world=1, rank=0, l
         ach = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         roof = {"kernel": dominant, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
+    tot_ms = sum(v["total_ms"] for v in fams.values())
     roof.update({"avg_launch_us": round(avg_ms * 1e3, 2), "alg_bytes_per_launch": bytes_per_launch,
-                 "launches": d["launches"], "epoch_alg_GBps": round(alg / dt / 1e9, 1),
-                 "epoch_alg_bytes": alg / max(1, steps)})
+                 "launches": d["launches"], "share_of_kernel_time": round(d["total_ms"] / max(1e-9, tot_ms), 3),
+                 "epoch_alg_GBps": round(alg / dt / 1e9, 1), "epoch_alg_bytes": alg / max(1, steps),
+                 "families_ms_per_epoch": {kk: round(v["total_ms"] / steps, 3) for kk, v in
+                                           sorted(fams.items(), key=lambda kv: -kv[1]["total_ms"])[:6]}})
     # HBM bytes per launch of the same kernel family from the committed
     # rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, MI355X guide §HBM).
     pat = f"r*_{pmc_tag}pmc_traffic.json"
@@ -158,11 +191,27 @@ def run_newton(ds, prec, steps, warmup, k=32, self_side=True, world=1, rank=0, l
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and "--gpus" in " ".join(sys.argv):
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if world > 1:
         dist.init_process_group("gloo")
+    if os.environ.get("OCFFM_BENCH_DRY") == "1":
+        # launcher check (CPU tests): every rank reports in, nothing touches the GPU
+        t = torch.tensor([1.0])
+        if world > 1:
+            dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"n_gpus": world, "ranks_seen": int(t.item()),
+                              "launcher": os.environ.get("OCFFM_BENCH_LAUNCHER", "torchrun" if world > 1 else "none")}),
+                  flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     prec = ocffm.FP32 if args.precision == "fp32" else ocffm.FP64
 
     ds = synth.kkbox(m=ROWS_PER_GPU * world)
@@ -184,21 +233,31 @@ def main():
         # N = 1 on the multi-rank code path (a one-rank RCCL communicator):
         # the compute cost of that path without any real exchange
         comm = ocffm.comm_id()
+    snap = {}
+    want_cpu = rank == 0 and world == 1 and args.cpu_baseline == "auto"
+
+    def take(g):  # the GPU's tables after the warm-up: the CPU baseline starts there
+        fu = int(ds.train.fid.max()) + 1
+        fv = int(ds.item.fid.max()) + 1
+        snap["tables"] = {(w, b): g.get(w, b) for b in _blocks(fu, fv) for w in "WH"}
+        snap["epoch"] = max(1, args.warmup) + 1
+
     r = run_newton(ds, prec, args.steps, args.warmup, k=32, world=world, rank=rank, local=local, comm=comm,
-                   allreduce=allreduce, pmc_tag="" if prec == ocffm.FP32 else "fp64_")
+                   allreduce=allreduce, pmc_tag="" if prec == ocffm.FP32 else "fp64_",
+                   snapshot=take if want_cpu else None)
     rows_total = ROWS_PER_GPU * world
     value = rows_total * args.steps / r["dt"]
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_baseline == "auto":
-        cpu = cpu_baseline(ds, args.cpu_epochs, args.cpu_single_epochs)
+    if want_cpu:
+        cpu = cpu_baseline(ds, args.cpu_epochs, args.cpu_single_epochs, snap, r["cg_per_epoch"])
     modes = {}
     if world == 1 and args.modes == "auto":
         if prec == ocffm.FP32:
-            modes["fp64"] = fp64_mode(ds, args)
-        modes["cfg5"] = cfg5_mode(args)
+            modes["fp64"] = timed_mode(fp64_mode, ds, args)
+        modes["cfg5"] = timed_mode(cfg5_mode, args)
         if args.sgd == "auto":
-            modes["sgd"] = sgd_mode(ds, args)
+            modes["sgd"] = timed_mode(sgd_mode, ds, args)
 
     if rank == 0:
         line = {
@@ -212,6 +271,9 @@ def main():
                        "positives": ds.n_positives, "user_fields": 2, "item_fields": 3, "k": 32,
                        "lambda": 4.0, "omega": 0.0078125, "r": -1.0,
                        "parallelism": f"dp{world}" + ("-rccl1" if comm is not None and world == 1 else ""),
+                       "rccl_ranks": world if comm is not None else 0,
+                       "launcher": os.environ.get("OCFFM_BENCH_LAUNCHER", "torchrun" if world > 1 else "none"),
+                       "allreduce": "gloo-host (rehearsal)" if rehearsal else ("rccl" if comm is not None else "none"),
                        "cg_iters_per_epoch": r["cg_per_epoch"]},
             "roofline": r["roof"],
             "cpu_baseline": cpu,
@@ -221,6 +283,22 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _blocks(fu, fv, self_side=True):
+    """index_vec (ffm.cpp:53-55) of every block of the model."""
+    f = fu + fv
+    return [f2 + (f - 1) * f1 - f1 * (f1 - 1) // 2 for f1 in range(f) for f2 in range(f1, f)
+            if self_side or (f1 < fu <= f2)]
+
+
+def timed_mode(fn, *a):
+    """A mode's result with its wall time and the process's peak host RSS."""
+    t0 = time.perf_counter()
+    out = fn(*a)
+    out["wall_s"] = round(time.perf_counter() - t0, 1)
+    out["peak_rss_GB"] = round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6, 2)
+    return out
 
 
 def fp64_mode(ds, args):
@@ -244,18 +322,21 @@ def cfg5_mode(args):
     Cache).  Weak scaling at N GPUs = N such shards."""
     try:
         t0 = time.perf_counter()
-        ds = synth.cfg5(m=CFG5_ROWS)
+        rows = args.cfg5_rows
+        ds = synth.cfg5(m=rows)
         gen = time.perf_counter() - t0
         steps = max(1, min(args.steps, args.cfg5_steps))
         r = run_newton(ds, ocffm.FP32, steps, 1, k=64, self_side=False, pmc_tag="cfg5_")
         return {"metric": "train instances/sec, config-5 shard (39+1 fields, 250k feats/field, k=64, --ns)",
-                "value": round(CFG5_ROWS * steps / r["dt"], 1), "unit": "instances/s", "dtype": "f32",
+                "value": round(rows * steps / r["dt"], 1), "unit": "instances/s", "dtype": "f32",
                 "steps": steps, "ms_per_step": round(r["dt"] / steps * 1e3, 3),
-                "config": {"workload": "BASELINE configs[4] restated (SURVEY §8d): one GPU's row shard",
-                           "rows_per_gpu": CFG5_ROWS, "items": int(ds.item.m), "positives": ds.n_positives,
+                "config": {"workload": "BASELINE configs[4] restated (SURVEY §8d): one GPU's row shard "
+                                       "(100 M rows / 8 GPUs)" if rows == CFG5_ROWS else
+                                       f"BASELINE configs[4] structure, {rows} rows (not the 8-GPU shard)",
+                           "rows_per_gpu": rows, "items": int(ds.item.m), "positives": ds.n_positives,
                            "user_fields": 39, "item_fields": 1, "features_per_field": 250000, "k": 64,
                            "self_side": False, "cg_iters_per_epoch": r["cg_per_epoch"],
-                           "p_cache_GB": round(39 * CFG5_ROWS * 64 * 4 / 1e9, 1), "datagen_s": round(gen, 1),
+                           "p_cache_GB": round(39 * rows * 64 * 4 / 1e9, 1), "datagen_s": round(gen, 1),
                            "setup_s": r["setup_s"]},
                 "roofline": r["roof"]}
     except Exception as e:  # never blocks the headline number
@@ -293,23 +374,51 @@ def sgd_mode(ds, args):
         return {"value": None, "error": str(e)}
 
 
-def cpu_baseline(ds, epochs, single_epochs=1):
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(ds, epochs, single_epochs=1, snap=None, gpu_cg=None):
     """The CPU oracle on a bounded sample: `epochs` epochs of the same
-    kkbox-shaped problem, fp64, all host threads this process may use."""
+    kkbox-shaped problem, fp64, on every host core this process may use.
+    With `snap` (the GPU's tables after its warm-up) the oracle starts from
+    that state, so its sample is the same epoch window as the GPU's first
+    timed epochs (later epochs need fewer CG steps than the first ones)."""
     try:
         import oracle_lib as O
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        avail = len(os.sched_getaffinity(0))
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or avail
         o = O.Oracle(ds, threads=threads, with_test=False)
         ocffm.srand(1)
         o.init()
+        window = "epochs 1.." + str(epochs) + " from init"
+        if snap and "tables" in snap:
+            for (w, b), t in snap["tables"].items():
+                o.set(w, b, t)
+            o.refresh()
+            window = f"epochs {snap['epoch']}..{snap['epoch'] + epochs - 1} (from the GPU's tables after its warm-up)"
+        o.cg_log_clear()
         secs = o.time_epochs(epochs, threads)
+        cg = float(o.cg_log().sum()) / max(1, epochs)
         out = {"value": round(ds.train.m * epochs / secs, 1), "unit": "instances/s", "cores": threads,
                "kind": "port", "precision": "f64",
-               "sample": f"{epochs} epoch(s) of the same kkbox-shape problem ({ds.train.m} rows), {secs:.2f} s"}
+               "sample": f"{epochs} epoch(s) of the same kkbox-shape problem ({ds.train.m} rows), {window}, "
+                         f"{secs:.2f} s",
+               "cg_iters_per_epoch": round(cg, 1), "gpu_cg_iters_per_epoch": gpu_cg,
+               "host": {"cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count(), "affinity_cpus": avail,
+                        "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}}
+        if gpu_cg:  # the same rate per CG step (the work an epoch does scales with its CG steps)
+            out["value_at_gpu_cg_count"] = round(out["value"] * cg / gpu_cg, 1)
         if single_epochs > 0:  # SURVEY 8(d): also the one-thread rate (the reference's -c 1)
             s1 = o.time_epochs(single_epochs, 1)
             out["single_thread"] = {"value": round(ds.train.m * single_epochs / s1, 1), "cores": 1,
-                                    "sample": f"{single_epochs} epoch(s), {s1:.2f} s"}
+                                    "sample": f"{single_epochs} epoch(s) after the sample above, {s1:.2f} s"}
         return out
     except Exception as e:  # the baseline never blocks the GPU number
         return {"value": None, "unit": "instances/s", "cores": 0, "kind": "port", "sample": f"failed: {e}"}

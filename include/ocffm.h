@@ -162,9 +162,14 @@ int ocffm_problem_validate(ocffm_problem *p, ocffm_metrics *out);
 /* The reference's nDCG known-answer build (-DEBUG_nDCG -DSHOW_SCORE_ONLY,
  * script/nDCG_degub_tool/readme:1-4): validate() with every test row's
  * scores forced to z_j = n - j after its ploss term (ffm.cpp:988-993).
- * per_row_ndcg10 (optional): the nDCG@10 of each of this rank's test rows,
- * the value that build prints per row (ffm.cpp:1126). */
-int ocffm_problem_validate_forced(ocffm_problem *p, ocffm_metrics *out, double *per_row_ndcg10);
+ * per_row_ndcg (optional, room for cap doubles): nDCG@5,10,20,40,80 of each
+ * of this rank's test rows, row-major (ffm.cpp:1059-1128; the build prints
+ * the @10 value per row, ffm.cpp:1126).  OCFFM_E_ARG when cap < 5 x
+ * ocffm_problem_test_rows(). */
+int ocffm_problem_validate_forced(ocffm_problem *p, ocffm_metrics *out, double *per_row_ndcg, uint64_t cap);
+/* Test rows of this rank (Uva->m of the reference, ffm.cpp:925; 0 without a
+ * test set). */
+int ocffm_problem_test_rows(ocffm_problem *p, uint64_t *m);
 
 /* print_epoch_info (ffm.cpp:1130-1145) of the last validation, and the
  * header of init_va (ffm.cpp:901-912), to stdout. */

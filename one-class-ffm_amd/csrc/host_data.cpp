@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <exception>
+#include <mutex>
 #include <random>
 #include <stdexcept>
 #include <string>
@@ -301,7 +302,11 @@ void build(HostData &d, Rows &&r) {
 
 // split_fields (ffm.cpp:185-257) + popularity (ffm.cpp:143,172-176) on the
 // host: the checker of the device build and the input of the host consumers.
+// Consumers on several threads may share one data set (per-GPU problems
+// created concurrently): the lazy split runs under one lock, once.
 const HostData &split_host(const HostData &d) {
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
   if (d.split_done) return d;
   const Rows &r = d.raw;
   if (d.has_label) {

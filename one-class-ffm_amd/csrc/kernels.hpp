@@ -510,6 +510,11 @@ template <typename real> struct Fin {
   // would then associate differently from run to run.  nhd: slots (0: none).
   double *hdots;
   uint32_t nhd;
+  // Exact residual (fp64 parity mode, OCFFM_EXACT_R2): the finalisation
+  // publishes alpha only; k_cg_r2 then reduces |r - alpha Hp|^2 as a second
+  // pass, as ffm.cpp:807-808 recomputes |R|^2 after R -= alpha Hv, and
+  // publishes beta and the verdict.
+  int exact_r2;
 };
 
 // MODE 0 (gradient, ffm.cpp:561-570, 773-779): G = lam f W + s; r = -G;
@@ -601,9 +606,13 @@ __device__ __forceinline__ void cg_publish(const Fin<real> &f, const double (&to
   } else {
     const double r2 = st->r2;
     const double alpha = r2 / tot[0];
-    const double r2n = r2 - 2 * alpha * tot[1] + alpha * alpha * tot[2];
     st->vhv = tot[0];
     st->alpha = alpha;
+    if (f.exact_r2) {  // beta, r2 and the verdict: k_cg_r2
+      st->nr_cg = f.it;
+      return;
+    }
+    const double r2n = r2 - 2 * alpha * tot[1] + alpha * alpha * tot[2];
     st->beta = r2n / r2;
     st->r2 = r2n;
     st->nr_cg = f.it;
@@ -1632,6 +1641,35 @@ __global__ __launch_bounds__(BLOCK) void k_fin(uint64_t nv, Fin<real> f) {
     col_finalize<real, KP, MODE>(f, (uint32_t)(v / G::LPR), s, alpha, beta, upd, (int)(v % G::LPR), dsum);
   }
   fin_blocks<real, MODE>(f, dsum);
+}
+
+// Exact CG residual (Fin::exact_r2): after the finalisation of iteration
+// f.it has published alpha, |r - alpha Hp|^2 over the D x KP vectors in a
+// fixed order (grid-stride, block tree, block order), then beta = r2n / r2
+// and the verdict of iteration it+1 (ffm.cpp:807-809).  r and Hp hold
+// iteration it's values here: the lazy update (cg_dir_at) applies
+// r -= alpha Hp in the next feature pass, with this same rounding.
+template <typename real>
+__global__ __launch_bounds__(BLOCK) void k_cg_r2(uint64_t nv, Fin<real> f) {
+  CgState *st = f.st;
+  if (!st->run[f.it]) return;
+  const real alpha = (real)st->alpha;
+  double acc = 0;
+  VEC_LOOP {
+    const vec_t<real> rn = vld<real>(f.R + v * VT<real>::N) - vsplat<real>(alpha) * vld<real>(f.Hp + v * VT<real>::N);
+#pragma unroll
+    for (int e = 0; e < VT<real>::N; e++) acc += (double)rn[e] * (double)rn[e];
+  }
+  double bv[1] = {block_sum(acc)}, tot[1];
+  if (last_block<1>(bv, f.part, f.tick, tot) && threadIdx.x == 0) {
+    const double r2 = st->r2, r2n = tot[0];
+    st->beta = r2n / r2;
+    st->r2 = r2n;
+    const int go = (f.it < MAXCG && st->g2 * CG_EPS < r2n) ? 1 : 0;
+    st->run[f.it + 1] = go;
+    if (f.run_host)
+      __hip_atomic_store(f.run_host + f.it + 1, go ? RUN_GO : RUN_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // The step of the half: S += alpha_last p_last (the update of the last CG

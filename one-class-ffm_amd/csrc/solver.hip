@@ -279,7 +279,8 @@ struct ProblemBase {
   virtual void one_epoch() = 0;
   virtual void solve_block(uint32_t f1, uint32_t f2) = 0;
   virtual void cache_sasb() = 0;
-  virtual void validate(ocffm_metrics *m, bool forced = false, double *per_row_ndcg10 = nullptr) = 0;
+  virtual void validate(ocffm_metrics *m, bool forced = false, double *per_row_ndcg = nullptr, uint64_t cap = 0) = 0;
+  virtual uint64_t test_rows() const = 0;
   virtual uint64_t get(char what, uint32_t b12, double *out, uint64_t cap) = 0;
   virtual void set(char what, uint32_t b12, const double *in, uint64_t len) = 0;
   virtual void grad(uint32_t f1, uint32_t f2, int half, double *out) = 0;
@@ -405,7 +406,12 @@ template <typename real> class Problem final : public ProblemBase {
     dots_.alloc(4);
     bsum_.alloc(2);
     ysum_.alloc(std::max<uint64_t>(std::max(U_.nseg, V_.nseg), 1));
-    if (tpre(Rmax)) Tpre_.alloc(Rmax * kp_);
+    // T pre-pass rows: the larger side that takes the pre-pass (tpre() also
+    // bounds R for 32-bit buffer offsets, so test each side on its own)
+    uint64_t tR = 0;
+    for (const uint64_t R : {U_.R, V_.R})
+      if (tpre(R)) tR = std::max(tR, R);
+    if (tR) Tpre_.alloc(tR * kp_);
   }
 
   ~Problem() override {
@@ -418,6 +424,7 @@ template <typename real> class Problem final : public ProblemBase {
   }
 
   bool has_test() const override { return has_test_; }
+  uint64_t test_rows() const override { return has_test_ ? T_.R : 0; }
   uint32_t nr_pass() const override { return prm_.nr_pass; }
   int rank() const override { return comm_.rank; }
   void sync() override { HIPCHK(hipStreamSynchronize(stream_)); }
@@ -598,6 +605,10 @@ template <typename real> class Problem final : public ProblemBase {
   // a/b and y~ as init does.  The result is the state init() would reach if
   // its draw had produced these tables.
   void load_binary(const std::string &path) override {
+    // The whole file is read and checked into host buffers first (header,
+    // field sizes, every block's table, no trailing bytes); the device
+    // state is touched only after that, so a bad or short file leaves the
+    // problem exactly as it was.
     std::FILE *fp = std::fopen(path.c_str(), "rb");
     if (!fp) throw Error(OCFFM_E_IO, "cannot read " + path);
     std::unique_ptr<std::FILE, int (*)(std::FILE *)> guard(fp, &std::fclose);
@@ -612,10 +623,7 @@ template <typename real> class Problem final : public ProblemBase {
     get_(du.data(), fu_ * sizeof(uint64_t));
     get_(dv.data(), fv_ * sizeof(uint64_t));
     if (du != U_.Ds || dv != V_.Ds) throw Error(OCFFM_E_DATA, "binary model: field sizes differ from this problem");
-    ysum_dirty();
-    excl_ = ExclBase{};
-    lazy_ok_ = false;
-    std::vector<double> w;
+    std::vector<std::pair<uint32_t, std::vector<double>>> tabs;  // (b12, W or H), file order
     for (uint32_t f1 = 0; f1 < f_; f1++)
       for (uint32_t f2 = f1; f2 < f_; f2++) {
         const uint32_t b12 = block_index(f1, f2, f_);
@@ -625,25 +633,35 @@ template <typename real> class Problem final : public ProblemBase {
         get_(&idx, sizeof(idx));
         get_(&nw, sizeof(nw));
         get_(&nh, sizeof(nh));
-        DevSide<real> &s1 = side(f1), &s2 = side(f2);
-        const uint64_t D1 = s1.Ds[fidx(f1)], D2 = s2.Ds[fidx(f2)];
+        const uint64_t D1 = side(f1).Ds[fidx(f1)], D2 = side(f2).Ds[fidx(f2)];
         if (idx != b12 || nw != D1 * k_ || nh != D2 * k_) throw Error(OCFFM_E_DATA, "binary model: block table differs");
-        for (int t = 0; t < 2; t++) {
-          const uint64_t D = t == 0 ? D1 : D2;
-          w.resize(D * k_);
-          get_(w.data(), w.size() * sizeof(double));
-          DevBuf<real> &dst = t == 0 ? W_[b12] : H_[b12];
-          if (!dst.p) dst.alloc(D * kp_);
-          std::vector<real> pad(D * kp_, (real)0);
-          for (uint64_t rr = 0; rr < D; rr++)
-            for (uint32_t cc = 0; cc < k_; cc++) pad[rr * kp_ + cc] = (real)w[rr * k_ + cc];
-          HIPCHK(hipMemcpy(dst.p, pad.data(), pad.size() * sizeof(real), hipMemcpyHostToDevice));
+        for (const uint64_t n : {nw, nh}) {
+          tabs.emplace_back(b12, std::vector<double>(n));
+          get_(tabs.back().second.data(), n * sizeof(double));
         }
-        if (!P_[b12].p) P_[b12].alloc(std::max<uint64_t>(s1.R, 1) * kp_);
-        if (!Q_[b12].p) Q_[b12].alloc(std::max<uint64_t>(s2.R, 1) * kp_);
-        utx(s1, fidx(f1), W_[b12].p, P_[b12].p);
-        utx(s2, fidx(f2), H_[b12].p, Q_[b12].p);
       }
+    if (std::fgetc(fp) != EOF) throw Error(OCFFM_E_DATA, "binary model: trailing bytes after the last block");
+    ysum_dirty();
+    excl_ = ExclBase{};
+    lazy_ok_ = false;
+    for (size_t q = 0; q < tabs.size(); q++) {
+      const uint32_t b12 = tabs[q].first;
+      const Block &b = blocks_[b12];
+      const bool isW = q % 2 == 0;
+      const uint32_t fl = isW ? b.f1 : b.f2;
+      DevSide<real> &sd = side(fl);
+      const uint64_t D = sd.Ds[fidx(fl)];
+      const std::vector<double> &w = tabs[q].second;
+      DevBuf<real> &dst = isW ? W_[b12] : H_[b12];
+      if (!dst.p) dst.alloc(D * kp_);
+      std::vector<real> pad(D * kp_, (real)0);
+      for (uint64_t rr = 0; rr < D; rr++)
+        for (uint32_t cc = 0; cc < k_; cc++) pad[rr * kp_ + cc] = (real)w[rr * k_ + cc];
+      HIPCHK(hipMemcpy(dst.p, pad.data(), pad.size() * sizeof(real), hipMemcpyHostToDevice));
+      DevBuf<real> &proj = isW ? P_[b12] : Q_[b12];
+      if (!proj.p) proj.alloc(std::max<uint64_t>(sd.R, 1) * kp_);
+      utx(sd, fidx(fl), dst.p, proj.p);
+    }
     HIPCHK(hipMemsetAsync(U_.bias.p, 0, U_.bias.bytes(), stream_));
     HIPCHK(hipMemsetAsync(V_.bias.p, 0, V_.bias.bytes(), stream_));
     owned_stale_ = false;
@@ -766,9 +784,11 @@ template <typename real> class Problem final : public ProblemBase {
   // ------------------------------------------------------- validation
   // forced: the reference's nDCG debug build (EBUG_nDCG, ffm.cpp:988-993):
   // after the ploss term every row's scores become z_j = n - j; per_row
-  // (optional, this rank's test rows): nDCG@10 of each row (ffm.cpp:1126).
-  void validate(ocffm_metrics *out, bool forced = false, double *per_row = nullptr) override {
+  // (optional, this rank's test rows, cap doubles): nDCG@5,10,20,40,80 of
+  // each row, row-major (ffm.cpp:1059-1128; that build prints the @10 one).
+  void validate(ocffm_metrics *out, bool forced = false, double *per_row = nullptr, uint64_t cap = 0) override {
     need_init();
+    if (per_row && cap < test_rows() * 5) throw Error(OCFFM_E_ARG, "per-row nDCG buffer too small");
     sync_owned();
     static const uint32_t cuts[5] = {5, 10, 20, 40, 80};
     for (int s = 0; s < 5; s++) out->top_k[s] = cuts[s];
@@ -834,7 +854,8 @@ template <typename real> class Problem final : public ProblemBase {
     for (uint64_t i = 0; i < mt; i++)
       for (int x = 0; x < 11; x++) tot[x] += ro[i * 11 + x];
     if (per_row)
-      for (uint64_t i = 0; i < mt; i++) per_row[i] = ro[i * 11 + 7];
+      for (uint64_t i = 0; i < mt; i++)
+        for (int s = 0; s < 5; s++) per_row[i * 5 + s] = ro[i * 11 + 6 + s];
     allreduce_host(tot.data(), tot.size());
     const double mt_glob = (double)T_.R_glob;
     out->loss = std::sqrt(tot[0] / mt_glob);
@@ -1917,6 +1938,7 @@ template <typename real> class Problem final : public ProblemBase {
     f.tw = w_;
     f.hdots = nullptr;
     f.nhd = 0;
+    f.exact_r2 = exact_r2(h) ? 1 : 0;
     return f;
   }
   // Gram chunks of a one-node-per-row field (build_csc's column order): each
@@ -2123,8 +2145,21 @@ template <typename real> class Problem final : public ProblemBase {
     });
   }
 
-  // One Hessian-vector product lam*V + H(V) into Hv_ (+ alpha) for CG iteration `it`.
+  // One CG step: the Hessian-vector product lam*V + H(V) into Hv_ with alpha
+  // (and beta and the verdict, or those from the exact residual pass).
   void hv_pass(HalfCtx &h, int it) {
+    hv_product(h, it);
+    if (!exact_r2(h)) return;
+    const Fin<real> fin = make_fin(h, it);
+    const uint64_t nv = h.D * kp_ / (16 / sizeof(real));
+    prof_launch("cg_r2", (double)h.D * kp_ * sizeof(real) * 2,
+                [&] { launch(k_cg_r2<real>, grid_for(nv, BLOCK, 1024), BLOCK, 0, nv, fin); });
+  }
+  // Exact residual norm (fp64 parity mode): not for owned fields
+  // on several ranks, whose r / Hp rows are current on their owner only.
+  bool exact_r2(const HalfCtx &h) const { return exact_r2_ && !(comm_.active() && h.F->excl); }
+
+  void hv_product(HalfCtx &h, int it) {
     DevSide<real> &own = *h.own;
     const int *run = &st_.p->run[it];
     if (cgram(h)) {
@@ -2391,6 +2426,9 @@ template <typename real> class Problem final : public ProblemBase {
   // (k_seg_ysum); [0] user rows, [1] item rows.  OCFFM_YSUM=0: the passes
   // walk their positives every time.
   bool ysum_on_ = !std::getenv("OCFFM_YSUM") || std::atoi(std::getenv("OCFFM_YSUM")) != 0;
+  // CG residual |r|^2 recomputed by a second reduction (k_cg_r2) instead of
+  // the expanded scalar of the finalisation (OCFFM_EXACT_R2=1)
+  bool exact_r2_ = std::getenv("OCFFM_EXACT_R2") && std::atoi(std::getenv("OCFFM_EXACT_R2")) != 0;
   bool ysum_ok_[2] = {false, false};
   // Cross loop: the item halves read the block-excluded value through perm
   // from the user orientation (k_gd_cross_seg ytv) instead of a refresh after
@@ -2693,8 +2731,11 @@ int ocffm_problem_solve_block(ocffm_problem *prob, uint32_t f1, uint32_t f2) {
 }
 int ocffm_problem_cache_sasb(ocffm_problem *prob) { PROB_CALL(prob->p->cache_sasb()); }
 int ocffm_problem_validate(ocffm_problem *prob, ocffm_metrics *m) { PROB_CALL(prob->p->validate(m)); }
-int ocffm_problem_validate_forced(ocffm_problem *prob, ocffm_metrics *m, double *per_row_ndcg10) {
-  PROB_CALL(prob->p->validate(m, true, per_row_ndcg10));
+int ocffm_problem_validate_forced(ocffm_problem *prob, ocffm_metrics *m, double *per_row_ndcg, uint64_t cap) {
+  PROB_CALL(prob->p->validate(m, true, per_row_ndcg, cap));
+}
+int ocffm_problem_test_rows(ocffm_problem *prob, uint64_t *m) {
+  PROB_CALL(if (!m) throw Error(OCFFM_E_ARG, "null output"); *m = prob->p->test_rows());
 }
 int ocffm_problem_save_binary(ocffm_problem *prob, const char *path) { PROB_CALL(prob->p->save_binary(path)); }
 int ocffm_problem_load_binary(ocffm_problem *prob, const char *path) { PROB_CALL(prob->p->load_binary(path)); }

@@ -64,7 +64,7 @@ EXPORTS = [
     "ocffm_problem_solve_block", "ocffm_problem_cache_sasb", "ocffm_problem_solve",
     "ocffm_problem_validate", "ocffm_print_header", "ocffm_print_epoch", "ocffm_problem_get",
     "ocffm_problem_set", "ocffm_problem_grad", "ocffm_problem_hv", "ocffm_problem_save_model",
-    "ocffm_problem_validate_forced", "ocffm_problem_save_binary", "ocffm_problem_load_binary",
+    "ocffm_problem_validate_forced", "ocffm_problem_test_rows", "ocffm_problem_save_binary", "ocffm_problem_load_binary",
     "ocffm_problem_cg_log", "ocffm_problem_set_profiling", "ocffm_problem_set_profile_filter",
     "ocffm_problem_kernel_stats",
     "ocffm_problem_reset_stats", "ocffm_problem_alg_bytes", "ocffm_problem_sync",
@@ -113,7 +113,8 @@ def lib():
     L.ocffm_problem_grad.argtypes = [vp, u32, u32, i32, vp]
     L.ocffm_problem_hv.argtypes = [vp, u32, u32, i32, vp, vp]
     L.ocffm_problem_save_model.argtypes = [vp, C.c_char_p]
-    L.ocffm_problem_validate_forced.argtypes = [vp, C.POINTER(_Metrics), vp]
+    L.ocffm_problem_validate_forced.argtypes = [vp, C.POINTER(_Metrics), vp, u64]
+    L.ocffm_problem_test_rows.argtypes = [vp, C.POINTER(u64)]
     L.ocffm_problem_save_binary.argtypes = [vp, C.c_char_p]
     L.ocffm_problem_load_binary.argtypes = [vp, C.c_char_p]
     L.ocffm_problem_cg_log.argtypes = [vp, vp, i32, C.POINTER(C.c_int)]
@@ -413,13 +414,21 @@ class ImpProblem:
         _check(lib().ocffm_problem_validate(self.h, C.byref(m)))
         return dict(loss=m.loss, prec=np.array(m.prec[:]), ndcg=np.array(m.ndcg[:]), top_k=list(m.top_k))
 
-    def validate_forced(self, m_test: int):
+    def test_rows(self) -> int:
+        """This rank's test rows (0 without a test set)."""
+        n = C.c_uint64()
+        _check(lib().ocffm_problem_test_rows(self.h, C.byref(n)))
+        return int(n.value)
+
+    def validate_forced(self):
         """The reference's nDCG known-answer build (ffm.cpp:988-993): metrics
-        and the per-row nDCG@10 with the scores forced to z_j = n - j."""
+        and the per-row nDCG@5,10,20,40,80 (shape rows x 5) with the scores
+        forced to z_j = n - j."""
         m = _Metrics()
-        rows = np.zeros(max(1, m_test), dtype=np.float64)
-        _check(lib().ocffm_problem_validate_forced(self.h, C.byref(m), _ptr(rows)))
-        return dict(loss=m.loss, prec=np.array(m.prec[:]), ndcg=np.array(m.ndcg[:])), rows[:m_test]
+        mt = self.test_rows()
+        rows = np.zeros(max(1, mt) * 5, dtype=np.float64)
+        _check(lib().ocffm_problem_validate_forced(self.h, C.byref(m), _ptr(rows), rows.size))
+        return dict(loss=m.loss, prec=np.array(m.prec[:]), ndcg=np.array(m.ndcg[:])), rows[:mt * 5].reshape(mt, 5)
 
     def save_binary(self, path: str) -> None:
         _check(lib().ocffm_problem_save_binary(self.h, path.encode()))

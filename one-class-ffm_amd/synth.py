@@ -214,23 +214,38 @@ def cfg5(m: int = 2_000_000, n: int = 250_000, fu: int = 39, d_user: int = 250_0
     positives are drawn like kkbox's (uniform w.p. 1/2, else the Pareto head)."""
     rng = np.random.default_rng(seed)
     ptr, col = _positives(rng, m, n, mean_pos)
+    # one generator per (table, field), filled by a thread pool: numpy's
+    # bulk draws release the GIL, so the 12.5 M-row shard (BASELINE
+    # configs[4] / 8 GPUs: 487 M nodes) is drawn in seconds, not minutes
+    seeds = np.random.SeedSequence(seed + 1).spawn(2 * fu)
 
-    def user_fields(count):
+    def user_rows(count, table, lab_ptr, lab_col):
+        xptr = np.arange(count + 1, dtype=np.uint64) * np.uint64(fu)
+        fid = np.tile(np.arange(fu, dtype=np.uint32), count)
         ids = np.empty((count, fu), dtype=np.uint64)
-        for f in range(fu):
-            uni = rng.integers(0, d_user, size=count)
-            par = np.minimum(np.floor(rng.pareto(1.2, size=count)), d_user - 1).astype(np.int64)
-            # a field-specific permutation keeps the heads of different fields apart
-            par = (par * 7919 + f * 104729) % d_user
-            ids[:, f] = np.where(rng.random(count) < 0.5, uni, par)
-        return [(f, ids[:, f:f + 1], np.ones((count, 1))) for f in range(fu)]
 
-    train = _fast_rows(m, user_fields(m), ptr, col)
+        def field(f):
+            g = np.random.default_rng(seeds[table * fu + f])
+            for c0 in range(0, count, 1 << 22):
+                c = min(count - c0, 1 << 22)
+                uni = g.integers(0, d_user, size=c)
+                par = np.minimum(np.floor(g.pareto(1.2, size=c)), d_user - 1).astype(np.int64)
+                # a field-specific permutation keeps the heads of different fields apart
+                par = (par * 7919 + f * 104729) % d_user
+                ids[c0:c0 + c, f] = np.where(g.random(c) < 0.5, uni, par)
+
+        import concurrent.futures as cf
+        with cf.ThreadPoolExecutor(max_workers=max(1, min(16, os.cpu_count() or 1))) as ex:
+            list(ex.map(field, range(fu)))
+        return Rows(xptr, fid, ids.reshape(-1), np.ones(count * fu, dtype=np.float64),
+                    lab_ptr.astype(np.uint64), lab_col.astype(np.uint64))
+
+    train = user_rows(m, 0, ptr, col)
     item = _fast_rows(n, [(0, np.arange(n, dtype=np.uint64)[:, None], np.ones((n, 1)))])
     test = None
     if test_rows:
         tptr, tcol = _positives(rng, test_rows, n, mean_pos)
-        test = _fast_rows(test_rows, user_fields(test_rows), tptr, tcol)
+        test = user_rows(test_rows, 1, tptr, tcol)
     return Dataset(name, train, item, test, k=k,
                    params=dict(k=k, t=20, l=4.0, w=0.0078125, r=-1.0))
 

@@ -779,7 +779,8 @@ struct Problem {
 
   // ffm.cpp:925-1016.  `forced` reproduces the EBUG_nDCG debug build
   // (scores z_j = n - j) used by the nDCG known-answer test.
-  void validate(bool forced = false, Vec *per_row_ndcg10 = nullptr) {
+  // per_row_ndcg (optional): nDCG@top_k[s] of test row i at [i * nk + s].
+  void validate(bool forced = false, Vec *per_row_ndcg = nullptr) {
     if (Ut == nullptr) return;
     const u64 mt = Ut->m;
     const u32 nb = f * (f + 1) / 2;
@@ -811,7 +812,7 @@ struct Problem {
     std::vector<u64> hits(nk, 0);
     Vec nd(nk, 0);
     double ploss = 0;
-    if (per_row_ndcg10) per_row_ndcg10->assign(mt, 0.0);
+    if (per_row_ndcg) per_row_ndcg->assign(mt * nk, 0.0);
     for (u64 i = 0; i < mt; i++) {
       Vec z;
       if (Ut->nnx[i] == 0) {
@@ -840,7 +841,8 @@ struct Problem {
         hits[s] += h_row[s];
         nd[s] += nd_row[s];
       }
-      if (per_row_ndcg10 && nk > 1) (*per_row_ndcg10)[i] = nd_row[1];
+      if (per_row_ndcg)
+        for (u32 s = 0; s < nk; s++) (*per_row_ndcg)[i * nk + s] = nd_row[s];
     }
     loss = std::sqrt(ploss / (double)mt);
     for (u32 s = 0; s < nk; s++) {
@@ -1060,19 +1062,22 @@ void orc_set_threads(void *c, uint32_t t) {
   omp_set_num_threads((int)t);
 }
 
-// out: [loss, prec@5..80, ndcg@5..80] (11 doubles).
-void orc_validate(void *c, int forced, double *out, double *per_row_ndcg10) {
+// out: [loss, prec@5..80, ndcg@5..80] (11 doubles).  per_row_ndcg
+// (optional, cap doubles): nDCG@5,10,20,40,80 of each test row, row-major.
+// Returns the number of doubles per_row_ndcg needs (5 x test rows).
+uint64_t orc_validate(void *c, int forced, double *out, double *per_row_ndcg, uint64_t cap) {
   Problem &p = ((OrcCtx *)c)->prob;
   if (p.top_k.empty()) p.init_va(5);
   Vec rows;
-  p.validate(forced != 0, per_row_ndcg10 ? &rows : nullptr);
+  p.validate(forced != 0, per_row_ndcg ? &rows : nullptr);
   out[0] = p.loss;
   for (int s = 0; s < 5; s++) {
     out[1 + s] = p.va_prec[s];
     out[6 + s] = p.va_ndcg[s];
   }
-  if (per_row_ndcg10)
-    for (u64 i = 0; i < rows.size(); i++) per_row_ndcg10[i] = rows[i];
+  if (per_row_ndcg)
+    for (u64 i = 0; i < rows.size() && i < cap; i++) per_row_ndcg[i] = rows[i];
+  return p.Ut ? p.Ut->m * 5 : 0;
 }
 
 int orc_cg_log(void *c, int32_t *out, int cap) {

@@ -51,7 +51,8 @@ def lib():
         L.orc_func.restype = C.c_double
         L.orc_func.argtypes = [C.c_void_p]
         L.orc_set_threads.argtypes = [C.c_void_p, C.c_uint32]
-        L.orc_validate.argtypes = [C.c_void_p, C.c_int, _f64p, C.c_void_p]
+        L.orc_validate.argtypes = [C.c_void_p, C.c_int, _f64p, C.c_void_p, C.c_uint64]
+        L.orc_validate.restype = C.c_uint64
         L.orc_cg_log.restype = C.c_int
         L.orc_cg_log.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
         L.orc_cg_log_clear.argtypes = [C.c_void_p]
@@ -160,13 +161,15 @@ class Oracle:
         arr = np.ascontiguousarray(arr, dtype=np.float64)
         lib().orc_set(self.h, what.encode(), b12, arr, arr.size)
 
-    def validate(self, forced=False, per_row=False, m_test=0):
+    def validate(self, forced=False, per_row=False):
+        """per_row: also the nDCG@5,10,20,40,80 of every test row (rows x 5)."""
         out = np.zeros(11, dtype=np.float64)
-        rows = np.zeros(m_test, dtype=np.float64) if per_row else None
-        lib().orc_validate(self.h, int(forced), out, _ptr(rows))
+        need = lib().orc_validate(self.h, int(forced), out, None, 0) if per_row else 0
+        rows = np.zeros(max(1, need), dtype=np.float64) if per_row else None
+        lib().orc_validate(self.h, int(forced), out, _ptr(rows), need)
         res = dict(loss=out[0], prec=out[1:6].copy(), ndcg=out[6:11].copy())
         if per_row:
-            res["ndcg10_rows"] = rows
+            res["ndcg_rows"] = rows[:need].reshape(-1, 5)
         return res
 
     def cg_log(self):

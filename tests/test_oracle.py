@@ -1,14 +1,16 @@
 """CPU tests of the oracle itself: pin it before trusting it.
 
 1. The reference's only known-answer test (script/nDCG_degub_tool): with the
-   scores forced to z_j = n - j, nDCG@10 per row must equal gen_ans.py's
-   output (tests/golden/ndcg_kat/expected_ndcg10.txt, 4 d.p.).
+   scores forced to z_j = n - j, nDCG@5/10/20/40/80 per row must equal
+   gen_ans.py's ndcg() (tests/golden/ndcg_kat/expected_ndcg_*.txt, case1.mf
+   and user1.mf; and its own printout expected_ndcg10.txt, 4 d.p.).
 2. Math identities against the reference's own objective func()
    (ffm.cpp:1321-1351): the restated gradients (gd_side / gd_cross,
    ffm.cpp:537-703) equal finite differences of func, and the restated
    Hessian-vector products (hs_side / hs_cross + lambda*v, ffm.cpp:594-742)
    equal second differences (func is exactly quadratic in one table).
 """
+import ctypes as C
 import os
 
 import numpy as np
@@ -20,23 +22,37 @@ import synth
 GOLD = os.path.join(os.path.dirname(__file__), "golden", "ndcg_kat")
 
 
-def test_ndcg_known_answer():
-    import ctypes as C
+# (train file, test file): the readme's run (readme:10) and user1.mf as the
+# test rows (features 30-32 lie past the train Ds: those rows are cold)
+KAT_RUNS = [("case1.mf", "case1.mf"), ("case1.mf", "user1.mf"), ("user1.mf", "user1.mf")]
+TOP_K = (5, 10, 20, 40, 80)
+
+
+@pytest.mark.parametrize("train,test", KAT_RUNS)
+def test_ndcg_known_answer(train, test):
     L = O.lib()
-    U = O.data_read(os.path.join(GOLD, "case1.mf"), True)
+    U = O.data_read(os.path.join(GOLD, train), True)
     V = O.data_read(os.path.join(GOLD, "test_item.mf"), False)
-    Ut = O.data_read(os.path.join(GOLD, "case1.mf"), True, O.data_ds(U))
+    Ut = O.data_read(os.path.join(GOLD, test), True, O.data_ds(U))
     # readme:10 runs `train -k 8 -t 1 -p case1.mf test_item.mf case1.mf`
     h = L.orc_problem_new(U, Ut, V, 0.1, 1e-5, -1.0, 1, 8, 1, 1, 0)
     L.orc_srand(1)
     L.orc_init(h)
     out = np.zeros(11)
-    rows = np.zeros(20)
-    L.orc_validate(h, 1, out, rows.ctypes.data_as(C.c_void_p))
+    need = L.orc_validate(h, 1, out, None, 0)
+    rows = np.zeros(need)
+    L.orc_validate(h, 1, out, rows.ctypes.data_as(C.c_void_p), need)
     L.orc_problem_free(h)
-    expected = np.loadtxt(os.path.join(GOLD, "expected_ndcg10.txt"))
-    assert expected.shape == (20,)
-    np.testing.assert_array_equal(np.round(rows, 4), expected)
+    rows = rows.reshape(-1, 5)
+    # gen_ans.py's ndcg() at every k the build reports (full precision)
+    expected = np.loadtxt(os.path.join(GOLD, "expected_ndcg_" + test.replace(".mf", ".txt")))
+    assert rows.shape == expected.shape == (20, 5)
+    np.testing.assert_allclose(rows, expected, rtol=0, atol=1e-12)
+    # and gen_ans.py's own printout (nDCG@10, 4 d.p.) for the readme's run
+    if test == "case1.mf":
+        np.testing.assert_array_equal(np.round(rows[:, 1], 4), np.loadtxt(os.path.join(GOLD, "expected_ndcg10.txt")))
+    # the run's nDCG@k is the mean over the rows (ffm.cpp:1012-1015)
+    np.testing.assert_allclose(out[6:11], rows.mean(axis=0), rtol=0, atol=1e-12)
 
 
 def _small(self_side=True):

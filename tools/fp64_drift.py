@@ -1,0 +1,112 @@
+"""fp64 parity drift, measured (round-3 verdict item 1).
+
+For the sets whose fp64 parity had been held for one epoch only (k = 64 /
+100, the wide --ns set, the config-5 shape, heavy columns, outbrain shape),
+run E epochs of:
+  * the oracle at 1 thread (the checker) and twice at 8 threads — the
+    reference's own arithmetic reassociated (per-thread partial sums under
+    schedule(guided), ffm.cpp:557,759), i.e. the drift the reference allows
+    against itself;
+  * the GPU fp64 path with the expanded CG residual (default) and with the
+    exact one (OCFFM_EXACT_R2=1: |R|^2 recomputed after R -= alpha Hv, as
+    ffm.cpp:807-808).
+Prints, per set and epoch, the max relative state difference (W, H of every
+block) of each run against the 1-thread oracle, and whether the CG logs agree.
+
+    python tools/fp64_drift.py [epochs] [--json out.json]
+"""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "one-class-ffm_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+import numpy as np  # noqa: E402
+
+import oracle_lib as O  # noqa: E402
+import synth  # noqa: E402
+
+
+def rel(a, b):
+    return float(np.abs(a - b).max() / max(1e-300, np.abs(b).max())) if b.size else 0.0
+
+
+def names(o):
+    return [O.block_index(f1, f2, o.f) for f1 in range(o.f) for f2 in range(f1, o.f)
+            if o.self_side or (f1 < o.fu <= f2)]
+
+
+SETS = {
+    "k64": (lambda: synth.tiny(seed=4, m=300), dict(k=64)),
+    "k100": (lambda: synth.tiny(seed=4, m=300), dict(k=100)),
+    "wide_ns": (lambda: synth.general(seed=33, m=200, n=40, fu=39, fv=1, k=8, d_user=[20] * 39, d_item=[40],
+                                      mean_pos=3.0, test_rows=20, name="wide_ns"), dict(self_side=False)),
+    "cfg5_shape": (lambda: synth.general(seed=41, m=300, n=60, fu=39, fv=1, k=64, d_user=[50] * 39, d_item=[60],
+                                         mean_pos=4.0, test_rows=30, name="cfg5_small"), dict(self_side=False, k=64)),
+    "heavy": (lambda: synth.general(seed=13, m=1500, n=300, fu=2, fv=2, k=8, d_user=[1500, 3], d_item=[300, 2],
+                                    nnz_user=1, mean_pos=12.0, vals="real"), dict()),
+    "outbrain": (lambda: synth.general(seed=32, m=400, n=60, fu=2, fv=2, k=64, mean_pos=1.0, test_rows=40,
+                                       name="outbrain"), dict(k=64)),
+}
+
+
+def run_oracle(ds, kw, threads, E):
+    o = O.Oracle(ds, threads=threads, with_test=False, **kw)
+    O.lib().orc_srand(1)
+    o.init()
+    st = []
+    for _ in range(E):
+        o.one_epoch()
+        st.append({(w, b): o.get(w, b) for b in names(o) for w in "WH"})
+    return st, o.cg_log().copy(), o
+
+
+def run_gpu(ds, kw, E, exact):
+    import ocffm
+    if exact:
+        os.environ["OCFFM_EXACT_R2"] = "1"
+    else:
+        os.environ.pop("OCFFM_EXACT_R2", None)
+    g = ocffm.problem_from_dataset(ds, precision=ocffm.FP64, with_test=False, **kw)
+    ocffm.srand(1)
+    g.init()
+    o = O.Oracle(ds, with_test=False, **kw)
+    st = []
+    for _ in range(E):
+        g.one_epoch()
+        st.append({(w, b): g.get(w, b) for b in names(o) for w in "WH"})
+    cg = g.cg_log().copy()
+    g.close()
+    os.environ.pop("OCFFM_EXACT_R2", None)
+    return st, cg
+
+
+def main():
+    E = int(sys.argv[1]) if len(sys.argv) > 1 and not sys.argv[1].startswith("-") else 3
+    out = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
+    gpu = "--cpu-only" not in sys.argv
+    only = sys.argv[sys.argv.index("--sets") + 1].split(",") if "--sets" in sys.argv else list(SETS)
+    res = {}
+    for name in only:
+        mk, kw = SETS[name]
+        ds = mk()
+        ref, cg1, _ = run_oracle(ds, kw, 1, E)
+        runs = {"oracle_c8a": run_oracle(ds, kw, 8, E)[:2], "oracle_c8b": run_oracle(ds, kw, 8, E)[:2]}
+        if gpu:
+            runs["gpu_expanded"] = run_gpu(ds, kw, E, False)
+            runs["gpu_exact"] = run_gpu(ds, kw, E, True)
+        res[name] = {}
+        for rn, (st, cg) in runs.items():
+            d = [max(rel(st[e][key], ref[e][key]) for key in ref[e]) for e in range(E)]
+            res[name][rn] = {"rel_per_epoch": d, "cg_equal": bool(np.array_equal(cg, cg1))}
+            print(f"{name:11s} {rn:13s} " + " ".join(f"{x:.2e}" for x in d) + f"  cg_equal={res[name][rn]['cg_equal']}",
+                  flush=True)
+    if out:
+        with open(out, "w") as f:
+            json.dump({"epochs": E, "sets": res}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -167,6 +167,10 @@ def _dist_dataset(name):
         # rank); their cross halves take the column-tau term before the all-reduce
         return synth.general(seed=23, m=300, n=200, fu=2, fv=2, k=8, d_user=[300, 6], d_item=[200, 5],
                              nnz_user=1, mean_pos=5.0, test_rows=30, name="lowcard")
+    if name == "outbrain":
+        # BASELINE configs[3]'s data-parallel workload at test size (SURVEY
+        # §8d): fu = 2, fv = 2, k = 64, ~1 positive per row
+        return synth.general(seed=32, m=400, n=60, fu=2, fv=2, k=64, mean_pos=1.0, test_rows=40, name="outbrain")
     # a listener-id field (D = m): every feature belongs to one rank's rows,
     # so its CG vectors stay sharded and only dot products are summed
     return synth.kkbox(seed=5, m=300, n=400, mean=12.0, name="kkbox_dist")
@@ -200,7 +204,8 @@ def _gpu_worker(rank, port, out_dir, world, name="tiny"):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,env", [("tiny", {}), ("owned", {}), ("lowcard", {"OCFFM_CGRAM": "2"}),
-                                      ("lowcard", {"OCFFM_CGRAM": "2", "OCFFM_FUSE": "0"})])
+                                      ("lowcard", {"OCFFM_CGRAM": "2", "OCFFM_FUSE": "0"}), ("outbrain", {}),
+                                      ("outbrain", {"OCFFM_EXACT_R2": "1"})])
 def test_two_ranks_match_one_rank_on_gpu(name, env, monkeypatch):
     import ocffm
     for k, v in env.items():  # inherited by the spawned ranks

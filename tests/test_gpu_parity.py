@@ -3,12 +3,18 @@
 Tolerances (written here):
   fp64 mode  : state (W, H, P, Q, a, b, y~) and objective within 1e-9 relative
                of the oracle; CG iteration counts identical; p@k / nDCG@k
-               identical up to 1e-12.
+               identical up to 1e-12.  Where the reference's own arithmetic
+               drifts further on a set (ill-conditioned capped CG solves:
+               k = 64 / 100 from epoch 2, heavy real-valued columns), the bound
+               is 3x that measured drift: the oracle at 2..16 threads against
+               itself at 1 thread (tests/golden/fp64_envelope.json, made by
+               tools/fp64_drift.py --envelope; fp64_tol below).
   fp32 mode  : objective and ploss within 1e-3 relative, p@k and nDCG@k
                within 2e-2 absolute (SURVEY §8c measured fp32 drift).
 Init is bit-exact in both modes' source tables: W/H come from the same host
 rand() stream as the reference (ffm.cpp:71-78).
 """
+import json
 import os
 import subprocess
 
@@ -24,6 +30,17 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TRAIN = os.path.join(REPO, "one-class-ffm_amd", "train")
 ORACLE_TRAIN = os.path.join(REPO, "oracle", "oracle_train")
+
+
+_ENV = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fp64_envelope.json")))
+
+
+def fp64_tol(name, epochs):
+    """max(1e-9, 3 x the reference arithmetic's own drift on this set after
+    `epochs` epochs) — the oracle's reassociated sums (per-thread partials
+    under schedule(guided), ffm.cpp:557,759) against its 1-thread run."""
+    env = _ENV["sets"].get(name)
+    return 1e-9 if env is None else max(1e-9, 3.0 * env[epochs - 1])
 
 
 def pair(ds, precision=ocffm.FP64, self_side=True, freq=False, with_test=True, **kw):
@@ -232,17 +249,19 @@ def test_variants_fp64(variant):
         if variant == name:
             kw["k"] = k
     o, g = pair(ds, self_side=variant not in ("ns", "wide_ns"), freq=variant == "freq", **kw)
-    # k >= 64: one epoch.  In the second, block (1,1)'s W half runs into the
-    # 20-iteration CG cap (ffm.cpp:761) on this set, and that ill-conditioned
-    # solve amplifies the reassociated sums (DPP trees vs the oracle's loops)
-    # to ~4e-7 with identical CG counts (measured; epoch 1 is within 1e-12)
-    for e in range(1 if kw.get("k", 4) >= 64 else 2):
+    # three epochs.  At k = 64 / 100 block (1,1)'s W half runs into the
+    # 20-iteration CG cap (ffm.cpp:761) from epoch 2 on this set, and that
+    # ill-conditioned solve amplifies any reassociation: the reference's own
+    # arithmetic drifts ~1e-6 (k = 64) / ~8e-9 (k = 100) between thread
+    # counts there (fp64_envelope.json), so those epochs are held to 3x it
+    epochs = 3
+    for e in range(1, epochs + 1):
         o.one_epoch()
         g.one_epoch()
-    assert_state(o, g, 1e-9)
+        assert_state(o, g, fp64_tol(variant, e))
     np.testing.assert_array_equal(g.cg_log(), o.cg_log())
     vo, vg = o.validate(), g.validate()
-    assert abs(vg["loss"] - vo["loss"]) <= 1e-9 * abs(vo["loss"])
+    assert abs(vg["loss"] - vo["loss"]) <= fp64_tol(variant, epochs) * abs(vo["loss"])
     np.testing.assert_allclose(vg["ndcg"], vo["ndcg"], atol=1e-12)
 
 
@@ -255,14 +274,15 @@ def _cfg5_small(m=300, n=60, k=64, fu=39, seed=41, test_rows=30):
 
 
 def test_cfg5_shape_fp64():
-    """Config-5 structure at test size in the parity mode: one epoch of all
-    78 halves against the oracle within 1e-9, identical CG counts, and the
-    validation metrics (ffm.cpp:852-870, 630-703 with C = 39)."""
+    """Config-5 structure at test size in the parity mode: two epochs of all
+    78 halves against the oracle within 1e-9 after each, identical CG
+    counts, and the validation metrics (ffm.cpp:852-870, 630-703 with C = 39)."""
     ds = _cfg5_small()
     o, g = pair(ds, self_side=False, k=64)
-    o.one_epoch()
-    g.one_epoch()
-    assert_state(o, g, 1e-9)
+    for e in (1, 2):
+        o.one_epoch()
+        g.one_epoch()
+        assert_state(o, g, fp64_tol("cfg5_shape", e))
     np.testing.assert_array_equal(g.cg_log(), o.cg_log())
     vo, vg = o.validate(), g.validate()
     assert abs(vg["loss"] - vo["loss"]) <= 1e-9 * abs(vo["loss"])
@@ -330,15 +350,16 @@ def test_heavy_columns(precision, cgram, monkeypatch):
     monkeypatch.setenv("OCFFM_CGRAM", cgram)
     ds = synth.general(**HEAVY)
     o, g = pair(ds, precision=precision, with_test=False)
-    for _ in range(2):
+    for e in (1, 2):
         o.one_epoch()
         g.one_epoch()
+        if precision == ocffm.FP64:
+            # 500-row real-valued columns make these halves worse conditioned:
+            # the reference's own sums drift 1.5-3.3e-9 between thread counts
+            # here (fp64_envelope.json "heavy"), the bound is 3x that
+            assert_state(o, g, fp64_tol("heavy", e))
     if precision == ocffm.FP64:
-        # 500-row real-valued columns make these halves worse conditioned: the
-        # reassociated sums (wave-chunk order, expanded |r - a Hp|^2) drift to
-        # ~2e-9 relative after two epochs, so this case uses 1e-8.
         np.testing.assert_array_equal(g.cg_log(), o.cg_log())
-        assert_state(o, g, 1e-8)
     else:
         f_ref = o.func()
         o2 = O.Oracle(ds, with_test=False)

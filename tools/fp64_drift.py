@@ -10,10 +10,16 @@ run E epochs of:
   * the GPU fp64 path with the expanded CG residual (default) and with the
     exact one (OCFFM_EXACT_R2=1: |R|^2 recomputed after R -= alpha Hv, as
     ffm.cpp:807-808).
-Prints, per set and epoch, the max relative state difference (W, H of every
-block) of each run against the 1-thread oracle, and whether the CG logs agree.
+Prints, per set and epoch, the max relative state difference (W, H, P, Q of
+every block, a, b, both y~ orientations) of each run against the 1-thread oracle, and whether the CG logs agree.
 
     python tools/fp64_drift.py [epochs] [--json out.json]
+    python tools/fp64_drift.py [epochs] --envelope tests/golden/fp64_envelope.json
+
+--envelope (CPU only): the oracle at 2, 3, 4, 6, 8 and 16 threads, twice
+each; per set and epoch the largest drift from the 1-thread run is the
+envelope of the reference's own arithmetic, which the GPU parity tests use
+as their bound where it exceeds 1e-9 (tests/test_gpu_parity.py fp64_tol).
 """
 import json
 import os
@@ -52,6 +58,15 @@ SETS = {
 }
 
 
+def state(x, o=None):
+    """Everything the parity tests compare (assert_state): W, H, P, Q of every
+    block, the biases and both orientations of y~."""
+    o = o or x
+    st = {(w, b): x.get(w, b) for b in names(o) for w in "WHPQ"}
+    st.update({(w, 0): x.get(w) for w in "abuv"})
+    return st
+
+
 def run_oracle(ds, kw, threads, E):
     o = O.Oracle(ds, threads=threads, with_test=False, **kw)
     O.lib().orc_srand(1)
@@ -59,7 +74,7 @@ def run_oracle(ds, kw, threads, E):
     st = []
     for _ in range(E):
         o.one_epoch()
-        st.append({(w, b): o.get(w, b) for b in names(o) for w in "WH"})
+        st.append(state(o))
     return st, o.cg_log().copy(), o
 
 
@@ -76,15 +91,36 @@ def run_gpu(ds, kw, E, exact):
     st = []
     for _ in range(E):
         g.one_epoch()
-        st.append({(w, b): g.get(w, b) for b in names(o) for w in "WH"})
+        st.append(state(g, o))
     cg = g.cg_log().copy()
     g.close()
     os.environ.pop("OCFFM_EXACT_R2", None)
     return st, cg
 
 
+def envelope(E, path):
+    res = {}
+    for name, (mk, kw) in SETS.items():
+        ds = mk()
+        ref, cg1, _ = run_oracle(ds, kw, 1, E)
+        env = [0.0] * E
+        for th in (2, 3, 4, 6, 8, 16):
+            for _ in range(2):
+                st, cg, _ = run_oracle(ds, kw, th, E)
+                assert np.array_equal(cg, cg1), (name, th)
+                env = [max(env[e], max(rel(st[e][key], ref[e][key]) for key in ref[e])) for e in range(E)]
+        res[name] = env
+        print(f"{name:11s} " + " ".join(f"{x:.2e}" for x in env), flush=True)
+    with open(path, "w") as f:
+        json.dump({"epochs": E, "threads": [2, 3, 4, 6, 8, 16], "repeats": 2,
+                   "what": "max relative difference (W, H, P, Q, a, b, y~) of the oracle at T threads vs 1 thread, per epoch",
+                   "sets": res}, f, indent=1)
+
+
 def main():
     E = int(sys.argv[1]) if len(sys.argv) > 1 and not sys.argv[1].startswith("-") else 3
+    if "--envelope" in sys.argv:
+        return envelope(E, sys.argv[sys.argv.index("--envelope") + 1])
     out = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
     gpu = "--cpu-only" not in sys.argv
     only = sys.argv[sys.argv.index("--sets") + 1].split(",") if "--sets" in sys.argv else list(SETS)

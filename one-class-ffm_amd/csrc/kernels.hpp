@@ -253,6 +253,26 @@ __device__ __forceinline__ vec_t<real> sg_vecmat(const vec_t<real> &x, const rea
   return t;
 }
 
+// The same product as a rolled loop (a lane-index shuffle per component, a
+// few rows of M in flight): for a path that runs rarely inside a kernel
+// whose register budget belongs to another path (k_hs_cross_seg's hot rows).
+template <typename real, int KP>
+__device__ __forceinline__ vec_t<real> sg_vecmat_rolled(const vec_t<real> &x, const real *M, int li) {
+  using G = Geo<real, KP>;
+  const int base = (int)(threadIdx.x & 63) & ~(G::LPR - 1);
+  vec_t<real> t = vzero<real>();
+  constexpr int UNR = KP <= 32 ? 2 : 1;  // loads in flight vs the host kernel's 4 waves/SIMD budget
+#pragma unroll UNR
+  for (int l = 0; l < G::LPR; l++) {
+#pragma unroll
+    for (int c = 0; c < G::VE; c++) {
+      const real xe = __shfl(x[c], base + l, 64);
+      t += vsplat<real>(xe) * vld<real>(M + (size_t)(l * G::VE + c) * KP + li * G::VE);
+    }
+  }
+  return t;
+}
+
 // Lane-local vector-matrix accumulation for t = x M summed over several M
 // (fp32): lane li holds rows r = li*4 + e of x, so it adds x[e] * M[r][n] for
 // ALL n into u (no cross-lane broadcast per element), column pairs in packed
@@ -1330,9 +1350,10 @@ static __global__ __launch_bounds__(BLOCK) void k_col_gram32(uint64_t nchunks, c
   f16x acc;
 #pragma unroll
   for (int r = 0; r < 16; r++) acc[r] = 0.0f;
+  // branch-free (rows past n have weight and row zero): a per-MFMA branch
+  // made the compiler copy the accumulator between AGPRs and VGPRs each time
 #pragma unroll
-  for (int s = 0; s < CGRAM32_ROWS / 2; s++)
-    if (2 * s < n) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cv[s] * qv[s], qv[s], acc, 0, 0, 0);
+  for (int s = 0; s < CGRAM32_ROWS / 2; s++) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cv[s] * qv[s], qv[s], acc, 0, 0, 0);
   // D register r of lane l: element m = 8(r/4) + 4(l/32) + r%4, n = l%32
   float *out = jb.nparts <= 1 ? G + (size_t)jb.col * 1024 : gpart + (size_t)jb.slot * 1024;
 #pragma unroll
@@ -1357,6 +1378,185 @@ static __global__ __launch_bounds__(BLOCK) void k_gram_slot_sum(const Job *__res
       if (q0 + u < jb.nparts) acc += y[u];
   }
   reinterpret_cast<f4v *>(G + (size_t)jb.col * 1024)[threadIdx.x] = acc;
+}
+
+// ------------------------------------------- per-row Grams (cross) ---
+// Hot rows of a cross half: a row i with many positives has
+//   sum_{j in Omega_i} <phi_i, q_j> q_j = G_i phi_i,  G_i = sum_{j in Omega_i} q_j q_j^T
+// (hs_cross row body, ffm.cpp:715-738).  The partner table Q1 is fixed over
+// the half's CG steps, so G_i is built once per half and each step reads
+// k x k values for the row instead of gathering |Omega_i| partner rows (a
+// popular item's ~10^4 users; a heavy user's ~10^2 items).  Chunks
+// (Job: col = the row's Gram slot, nparts = chunks of the row, slot = the
+// partial slot, [b, e) = a range of the row's positives) sum into G, or into
+// ordered partial slots that k_hot_slot_sum adds in slot order after the
+// launch (deterministic).  HOT_NONE: a segment of a row without a Gram.
+constexpr uint32_t HOT_NONE = 0xffffffffu;
+
+// Per segment: the Gram slot of its row (or HOT_NONE).
+static __global__ __launch_bounds__(BLOCK) void k_hot_seg(uint64_t nseg, const Seg *__restrict__ segs,
+                                                   const uint32_t *__restrict__ row_slot, uint32_t *__restrict__ out) {
+  const uint64_t s = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (s < nseg) out[s] = row_slot[segs[s].row];
+}
+
+// Generic build (fp64, or any KP): one block per chunk, the chunk's partner
+// rows staged through LDS cgram_rows at a time, thread t owns elements
+// t, t + BLOCK, ... of the k x k sum.  wts (optional): a weight per position
+// (per-column cross Grams: x_i^2 of the position's row).
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_hot_gram(const Job *__restrict__ chunks, const uint32_t *__restrict__ ycol,
+                                                    const real *__restrict__ wts, const real *__restrict__ Q1,
+                                                    real *__restrict__ G, real *__restrict__ gpart) {
+  constexpr int CH = cgram_rows(KP, (int)sizeof(real));
+  constexpr int KK = KP * KP;
+  constexpr int NE = (KK + BLOCK - 1) / BLOCK;
+  __shared__ real qs[CH * KP];
+  __shared__ real ws[CH];
+  const Job jb = chunks[blockIdx.x];
+  real acc[NE];
+#pragma unroll
+  for (int e = 0; e < NE; e++) acc[e] = 0;
+  for (int64_t b0 = jb.b; b0 < jb.e; b0 += CH) {
+    const int n = (int)(jb.e - b0 < CH ? jb.e - b0 : CH);
+    __syncthreads();
+    for (int t = threadIdx.x; t < n * KP; t += BLOCK) qs[t] = Q1[(size_t)ycol[b0 + t / KP] * KP + t % KP];
+    for (int t = threadIdx.x; t < n; t += BLOCK) ws[t] = wts ? wts[b0 + t] : (real)1;
+    __syncthreads();
+    for (int r = 0; r < n; r++) {
+      const real c = ws[r];
+#pragma unroll
+      for (int e = 0; e < NE; e++) {
+        const int t = threadIdx.x + e * BLOCK;
+        if (t < KK) acc[e] += c * qs[r * KP + t / KP] * qs[r * KP + t % KP];
+      }
+    }
+  }
+  real *out = jb.nparts <= 1 ? G + (size_t)jb.col * KK : gpart + (size_t)jb.slot * KK;
+#pragma unroll
+  for (int e = 0; e < NE; e++) {
+    const int t = threadIdx.x + e * BLOCK;
+    if (t < KK) out[t] = acc[e];
+  }
+}
+
+// fp32 builds on MFMA (v_mfma_f32_32x32x2f32, the k_col_gram32 operand
+// layout: a row pair r = 2s + lane/32 is the K dimension, lane l holds
+// w_r q_r[l % 32] as the A and q_r[l % 32] as the B operand).  One wave per
+// chunk (the host cuts a long row or column into up to 64 chunks, so a
+// popular item's ~10^4 positions spread over many waves); the chunk's rows
+// 32 at a time: one coalesced load of their indices and weights, the row
+// loads all in flight, then 16 MFMAs alternating over two accumulator sets.
+// Small batches keep the kernel at ~70 VGPRs (KP = 32), so several waves
+// per SIMD hide each other's load latency (a software-pipelined 64-row
+// version at 232 registers ran 3x slower).  KP = 32: one 32 x 32 tile.
+// KP = 64: tiles 00, 01 and 11 (G is symmetric; tile 10 is stored as the
+// transpose of 01).
+constexpr int HOT_CHUNK_MAX = 256;
+template <int KP>
+__global__ __launch_bounds__(BLOCK) void k_hot_gram_mfma(uint64_t nchunks, const Job *__restrict__ chunks,
+                                                         const uint32_t *__restrict__ ycol,
+                                                         const float *__restrict__ wts,
+                                                         const float *__restrict__ Q1, uint64_t q1rows,
+                                                         float *__restrict__ G, float *__restrict__ gpart,
+                                                         const float *__restrict__ xsq, const float *__restrict__ QTQ,
+                                                         float w) {
+  static_assert(KP == 32 || KP == 64, "MFMA hot Grams: KP 32 or 64");
+  typedef float f16x __attribute__((ext_vector_type(16)));
+  constexpr int T = KP / 32, NT = T == 1 ? 1 : 3, NA = 2, HB = 32, NS = HB / 2;
+  const int lane = threadIdx.x & 63;
+  const uint64_t wv = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+  if (wv >= nchunks) return;
+  const Job jb = chunks[wv];
+  const BufView qb = buf_view(Q1, q1rows * KP * 4);
+  const int e = lane & 31, hf = lane >> 5;
+  f16x acc[NA][NT];
+#pragma unroll
+  for (int u = 0; u < NA; u++)
+#pragma unroll
+    for (int a = 0; a < NT; a++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) acc[u][a][r] = 0.0f;
+  for (int64_t b0 = jb.b; b0 < jb.e; b0 += HB) {
+    const int n = (int)(jb.e - b0 < HB ? jb.e - b0 : HB);
+    const uint32_t il = lane < n ? ycol[b0 + lane] : 0u;
+    const float wl = lane < n ? (wts ? wts[b0 + lane] : 1.0f) : 0.0f;
+    float q0[NS], q1[T == 1 ? 1 : NS], w[NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+      const int r = 2 * s + hf;  // rows past n read zero (buffer range check)
+      const uint32_t i = (uint32_t)__shfl((int)il, r, 64);
+      w[s] = __shfl(wl, r, 64);
+      const uint32_t off = r < n ? i * (uint32_t)(KP * 4) + (uint32_t)e * 4u : 0xffffffffu;
+      q0[s] = bld1<float>(qb, off);
+      if constexpr (T == 2) q1[s] = bld1<float>(qb, r < n ? off + 128u : 0xffffffffu);
+    }
+    // branch-free: rows past n are zero (weight and row), so their MFMAs add
+    // nothing (a per-MFMA branch made the compiler copy the accumulators
+    // between AGPRs and VGPRs around every one of them)
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+      f16x(&c)[NT] = acc[s % NA];
+      const float a0 = w[s] * q0[s];
+      c[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, q0[s], c[0], 0, 0, 0);
+      if constexpr (T == 2) {
+        c[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, q1[s], c[1], 0, 0, 0);
+        c[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[s] * q1[s], q1[s], c[2], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 1; u < NA; u++)
+#pragma unroll
+    for (int a = 0; a < NT; a++) acc[0][a] += acc[u][a];
+  float *out = jb.nparts <= 1 ? G + (size_t)jb.col * KP * KP : gpart + (size_t)jb.slot * KP * KP;
+  // per-column cross Grams: the column tau w xsq_c QTQ, added once (by the
+  // column's first chunk; the slot sum carries it)
+  const float tw = (xsq && jb.flags == 0) ? w * xsq[jb.col] : 0.0f;
+  auto tau = [&](int m, int nn) { return xsq ? tw * QTQ[m * KP + nn] : 0.0f; };
+  // D register r of lane l: element m = 8(r/4) + 4(l/32) + r%4, n = l%32
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const int m = 8 * (r >> 2) + 4 * hf + (r & 3);
+    out[m * KP + e] = acc[0][0][r] + tau(m, e);
+    if constexpr (T == 2) {
+      out[m * KP + 32 + e] = acc[0][1][r] + tau(m, 32 + e);               // tile 01: rows 0..31, columns 32..63
+      out[(32 + e) * KP + m] = acc[0][1][r] + tau(32 + e, m);             // tile 10 = 01^T
+      out[(32 + m) * KP + 32 + e] = acc[0][2][r] + tau(32 + m, 32 + e);  // tile 11
+    }
+  }
+}
+
+// Per-column cross Grams: C_c += w xsq_c QTQ, the column tau
+// term folded in, so a CG step is C_c p_c alone (k_hv_cgram).
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_gram_add_tau(uint64_t D, real *__restrict__ G, const real *__restrict__ xsq,
+                                                        const real *__restrict__ QTQ, double w) {
+  constexpr int KK = KP * KP;
+  for (uint64_t t = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; t < D * KK; t += (uint64_t)gridDim.x * BLOCK)
+    G[t] += (real)(w * (double)xsq[t / KK]) * QTQ[t % KK];
+}
+
+// G of a multi-chunk row = its partial slots summed in slot order (sums:
+// Job{col = Gram slot, nparts, slot = first partial slot}); one block per row.
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_hot_slot_sum(const Job *__restrict__ sums, const real *__restrict__ gpart,
+                                                        real *__restrict__ G) {
+  constexpr int KK = KP * KP, GB = 8;
+  const Job jb = sums[blockIdx.x];
+  for (int t = threadIdx.x; t < KK; t += BLOCK) {
+    const real *src = gpart + (size_t)jb.slot * KK + t;
+    real acc = src[0];
+    for (uint32_t q0 = 1; q0 < jb.nparts; q0 += GB) {
+      real y[GB];
+#pragma unroll
+      for (int u = 0; u < GB; u++) y[u] = q0 + u < jb.nparts ? src[(size_t)(q0 + u) * KK] : (real)0;
+#pragma unroll
+      for (int u = 0; u < GB; u++)
+        if (q0 + u < jb.nparts) acc += y[u];
+    }
+    G[(size_t)jb.col * KK + t] = acc;
+  }
 }
 
 // One CG step of a Gram side half: per column, the direction p_c of
@@ -1399,7 +1599,9 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
                                                         const int *__restrict__ run, const real *__restrict__ Rv,
                                                         const real *__restrict__ Hv, const CgState *st, int it,
                                                         const uint32_t *__restrict__ segd,
-                                                        const real *__restrict__ segx) {
+                                                        const real *__restrict__ segx,
+                                                        const uint32_t *__restrict__ hot_seg,
+                                                        const real *__restrict__ hotG) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP, OCFFM_HS_GB>;  // gathers per round (32: one round per <= 32-positive segment)
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real));
@@ -1419,16 +1621,24 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
   const int sg = lane / G::LPR, li = lane % G::LPR;
   const real cpos = (real)(1 - w);
   // Per segment: phi from the row's node(s), the partner-row gathers, tau.
-  auto seg_out = [&](const Seg &sgm, uint32_t d1, real x1) -> vec_t<real> {
+  // A hot row (hs != HOT_NONE) reads its Gram instead: its first segment
+  // stores (1 - w) G_i phi_i (+ tau), its other segments zero.
+  auto seg_out = [&](const Seg &sgm, uint32_t d1, real x1, uint32_t hs) -> vec_t<real> {
     const uint64_t i = sgm.row;
+    if (hs != HOT_NONE && !seg_first(sgm)) return vzero<real>();
     uint32_t jj[PP::UT];  // the first pass's columns go out with the phi gather
-    PP::load_cols(ycol, sgm.b, sgm.e, li, jj);
+    if (hs == HOT_NONE) PP::load_cols(ycol, sgm.b, sgm.e, li, jj);
     vec_t<real> phi = vzero<real>();
     if (segd) {  // one node per row: the segment carries it (no row indirection)
       phi = vsplat<real>(x1) * cg_dir_at<real, KP>(V, Rv, Hv, alpha, beta, upd, (size_t)d1 * KP + li * G::VE);
     } else {
       for (int64_t p = xptr[i]; p < xptr[i + 1]; p++)
         phi += vsplat<real>(xval[p]) * cg_dir_at<real, KP>(V, Rv, Hv, alpha, beta, upd, (size_t)xidx[p] * KP + li * G::VE);
+    }
+    if (hs != HOT_NONE) {
+      vec_t<real> out = vsplat<real>(cpos) * sg_vecmat_rolled<real, KP>(phi, hotG + (size_t)hs * KP * KP, li);
+      if (QTQ) out += vsplat<real>((real)w) * sg_vecmat_rolled<real, KP>(phi, Qp, li);
+      return out;
     }
     vec_t<real> ka = vzero<real>();
     for (int64_t p0 = sgm.b; p0 < sgm.e; p0 += PP::PW) {
@@ -1459,7 +1669,7 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
   const uint64_t stride = nwaves * G::NSG;
   uint64_t s = wave * G::NSG + sg;
   Seg nxt{0u, 0u, 0, 0};
-  uint32_t nd = 0;
+  uint32_t nd = 0, nh = HOT_NONE;
   real nx = 0;
   if (s < nseg) {
     nxt = segs[s];
@@ -1467,10 +1677,11 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
       nd = segd[s];
       nx = segx[s];
     }
+    if (hot_seg) nh = hot_seg[s];
   }
   for (; s < nseg; s += stride) {
     const Seg sgm = nxt;
-    const uint32_t d1 = nd;
+    const uint32_t d1 = nd, hs = nh;
     const real x1 = nx;
     if (s + stride < nseg) {
       nxt = segs[s + stride];
@@ -1478,8 +1689,9 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
         nd = segd[s + stride];
         nx = segx[s + stride];
       }
+      if (hot_seg) nh = hot_seg[s + stride];
     }
-    vst<real>(h + s * KP + li * G::VE, seg_out(sgm, d1, x1));
+    vst<real>(h + s * KP + li * G::VE, seg_out(sgm, d1, x1, hs));
   }
 }
 

@@ -27,6 +27,7 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <type_traits>
 #include <vector>
 
@@ -122,6 +123,14 @@ template <typename real> struct DevField {
   bool excl = false;
   std::vector<uint8_t> h_own;
   DevBuf<uint8_t> own;
+  // Per-column cross Grams (one node per row, few columns): the
+  // positions of the field's rows' positives in column order (partner row,
+  // (1 - w) x^2 of the position's row) and their Gram build chunks.
+  bool ccg_ready = false;
+  DevBuf<uint32_t> cpos;
+  DevBuf<real> cw;
+  DevBuf<Job> cchunks, csums;
+  uint64_t cslots = 0, cnpos = 0;
   DevBuf<uint32_t> segd;  // one: the node of each positive segment's row (no row indirection)
   DevBuf<real> segx;
   // host copies kept until the segment CSC is built
@@ -146,6 +155,12 @@ template <typename real> struct DevSide {
   uint64_t nseg = 0;      // positive segments (kernels.hpp: Seg)
   DevBuf<Seg> segs;
   DevBuf<uint32_t> segptr;
+  // Hot rows (kernels.hpp k_hot_gram*): rows with >= hot_min positives whose
+  // cross-half Hessian-vector rows read a k x k Gram of their partner rows
+  // (built once per cross half) instead of gathering them every CG step.
+  uint64_t nhot = 0, hslots = 0, hpos = 0;  // rows, partial slots, their positives
+  DevBuf<uint32_t> hot_seg;                  // per segment: the row's Gram slot or HOT_NONE
+  DevBuf<Job> hchunks, hsums;
 };
 
 // Split every row's positives into segments of at most `len` (rows without
@@ -406,6 +421,21 @@ template <typename real> class Problem final : public ProblemBase {
     dots_.alloc(4);
     bsum_.alloc(2);
     ysum_.alloc(std::max<uint64_t>(std::max(U_.nseg, V_.nseg), 1));
+    // hot rows (opt-in, DESIGN §7: measured no gain at kkbox shape and a
+    // loss at config 5): >= OCFFM_HOT positives, in halves whose last CG
+    // count was >= OCFFM_HOT_STEPS (default 0 with OCFFM_HOT set)
+    if (const char *e = std::getenv("OCFFM_HOT")) {
+      hot_min_ = std::strtoull(e, nullptr, 10);
+      hot_steps_ = 0;
+    }
+    if (const char *e = std::getenv("OCFFM_HOT_STEPS")) hot_steps_ = std::atoi(e);
+    if (C_ > 0 && hot_min_ > 0) {
+      hot_setup(U_);
+      hot_setup(V_);
+      const uint64_t nh = std::max(U_.nhot, V_.nhot), ns = std::max(U_.hslots, V_.hslots);
+      if (nh) hotG_.alloc(nh * kp_ * kp_, false);
+      if (ns) hotP_.alloc(ns * kp_ * kp_, false);
+    }
     // T pre-pass rows: the larger side that takes the pre-pass (tpre() also
     // bounds R for 32-bit buffer offsets, so test each side on its own)
     uint64_t tR = 0;
@@ -415,6 +445,7 @@ template <typename real> class Problem final : public ProblemBase {
   }
 
   ~Problem() override {
+    clear_graphs();
     if (run_host_) (void)hipHostFree(run_host_);
     if (stage_) (void)hipHostFree(stage_);
     if (dstage_) (void)hipHostFree(dstage_);
@@ -510,6 +541,7 @@ template <typename real> class Problem final : public ProblemBase {
   std::chrono::steady_clock::time_point tmark_t_;
 
   void init() override {
+    clear_graphs();
     ysum_dirty();
     // a previous epoch that threw inside the cross loop may have left the
     // block-excluded form on: the base is rebuilt below from scratch
@@ -641,6 +673,7 @@ template <typename real> class Problem final : public ProblemBase {
         }
       }
     if (std::fgetc(fp) != EOF) throw Error(OCFFM_E_DATA, "binary model: trailing bytes after the last block");
+    clear_graphs();
     ysum_dirty();
     excl_ = ExclBase{};
     lazy_ok_ = false;
@@ -971,7 +1004,10 @@ template <typename real> class Problem final : public ProblemBase {
       const uint32_t c0 = cross_slot(std::min(hc.fl, hc.fo), std::max(hc.fl, hc.fo));
       qtq_ = M_.p + (size_t)c0 * kp_ * kp_;
     }
+    ccg_now_ = ccg_eligible(hc) && ccg_mode_ == 2;
+    hot_now_ = hot_steps_ == 0;
     col_grams(hc);
+    hot_grams(hc);
     // force iteration 1 to run
     CgState hs{};
     hs.run[1] = 1;
@@ -979,6 +1015,7 @@ template <typename real> class Problem final : public ProblemBase {
     sync();
     HIPCHK(hipMemcpy(st_.p, &hs, sizeof(CgState), hipMemcpyHostToDevice));
     hv_pass(hc, 1);
+    ccg_now_ = hot_now_ = false;
     sync();
     copy_out(Hv_.p, hc.D, out);
   }
@@ -1428,6 +1465,11 @@ template <typename real> class Problem final : public ProblemBase {
   template <typename... KArgs, typename... A>
   void launch(void (*k)(KArgs...), dim3 grid, dim3 block, size_t smem, A... a) {
     static_assert(sizeof...(KArgs) == sizeof...(A), "kernel argument count");
+    if (capturing_) {  // inside a hipGraph capture (graph mode, no profiling)
+      k<<<grid, block, smem, stream_>>>(static_cast<KArgs>(a)...);
+      HIPCHK(hipGetLastError());
+      return;
+    }
     hipEvent_t e0 = arm_first_ ? arm_a_ : nullptr;
     arm_first_ = false;
     hipExtLaunchKernelGGL(k, grid, block, (uint32_t)smem, stream_, e0, arm_b_, 0u, static_cast<KArgs>(a)...);
@@ -1941,6 +1983,95 @@ template <typename real> class Problem final : public ProblemBase {
     f.exact_r2 = exact_r2(h) ? 1 : 0;
     return f;
   }
+  // Gram build chunks of a list of position ranges (one Gram per range):
+  // ~HOT_CHUNK_MAX positions per chunk, at most 64 chunks per Gram; the
+  // chunks of a multi-chunk Gram write consecutive partial slots, summed in
+  // slot order by k_hot_slot_sum (sums: {gram, nparts, first slot}).
+  static void gram_chunks(const std::vector<std::pair<uint64_t, uint64_t>> &ranges, std::vector<Job> &chunks,
+                          std::vector<Job> &sums, uint64_t &slots, uint64_t cmax = HOT_CHUNK_MAX) {
+    for (uint64_t g = 0; g < ranges.size(); g++) {
+      const uint64_t b = ranges[g].first, e = ranges[g].second;
+      const uint64_t np = std::max<uint64_t>(1, std::min<uint64_t>(64, (e - b + cmax - 1) / cmax));
+      const uint64_t len = (e - b + np - 1) / std::max<uint64_t>(np, 1);
+      for (uint64_t q = 0; q < np; q++)
+        chunks.push_back(Job{(uint32_t)g, (uint32_t)np, np > 1 ? (uint32_t)(slots + q) : 0u, (uint32_t)q,
+                             (int64_t)std::min(e, b + q * len), (int64_t)std::min(e, b + (q + 1) * len)});
+      if (np > 1) {
+        sums.push_back(Job{(uint32_t)g, (uint32_t)np, (uint32_t)slots, 0u, 0, 0});
+        slots += np;
+      }
+    }
+    if (slots > 0xffffffffull) throw Error(OCFFM_E_DATA, "too many Gram partial slots");
+  }
+
+  // Hot rows of a side (rows with >= hot_min_ positives): Gram slots, the
+  // build chunks, and every segment's slot (k_hot_seg).
+  void hot_setup(DevSide<real> &s) {
+    if (!s.R || !s.npos) return;
+    std::vector<int64_t> yp(s.R + 1);
+    HIPCHK(hipMemcpy(yp.data(), s.yptr.p, yp.size() * sizeof(int64_t), hipMemcpyDeviceToHost));
+    std::vector<uint32_t> row_slot(s.R, HOT_NONE);
+    std::vector<std::pair<uint64_t, uint64_t>> ranges;
+    uint64_t nhot = 0, slots = 0, hpos = 0;
+    for (uint64_t i = 0; i < s.R; i++) {
+      const uint64_t b = (uint64_t)yp[i], e = (uint64_t)yp[i + 1];
+      if (e - b < hot_min_) continue;
+      row_slot[i] = (uint32_t)nhot;
+      ranges.emplace_back(b, e);
+      hpos += e - b;
+      nhot++;
+    }
+    if (!nhot) return;
+    std::vector<Job> chunks, sums;
+    gram_chunks(ranges, chunks, sums, slots);
+    s.nhot = nhot;
+    s.hslots = slots;
+    s.hpos = hpos;
+    s.hchunks.upload(chunks);
+    s.hsums.upload(sums);
+    DevBuf<uint32_t> rs;
+    rs.upload(row_slot);
+    s.hot_seg.alloc(s.nseg);
+    launch(k_hot_seg, (unsigned)((s.nseg + BLOCK - 1) / BLOCK), BLOCK, 0, (uint64_t)s.nseg, (const Seg *)s.segs.p,
+           (const uint32_t *)rs.p, s.hot_seg.p);
+    sync();
+  }
+  // A cross half reads hot rows' Grams when its previous CG count was at
+  // least hot_steps_ (the build is one MFMA pass over the hot positives;
+  // each step then saves their gathers) and it is not on column Grams.
+  bool hot(const HalfCtx &h) const { return hot_now_ && h.cross && h.own->nhot > 0 && hotG_.p && !ccg_now_; }
+
+  // The hot rows' Grams G_i = sum_{j in Omega_i} q_j q_j^T over this half's
+  // partner table (fixed over the half's CG steps).
+  void hot_grams(const HalfCtx &h) {
+    if (!hot(h)) return;
+    DevSide<real> &own = *h.own;
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      const double rs = sizeof(real);
+      const double bytes = (double)own.hpos * (4 + KP * rs) + (double)own.nhot * KP * KP * rs +
+                           (double)own.hslots * KP * KP * rs * 2;
+      prof_launch("hot_gram", bytes, [&] {
+        bool done = false;
+        if constexpr (std::is_same<real, float>::value && (KP == 32 || KP == 64)) {
+          if (!no_mfma_) {
+            launch(k_hot_gram_mfma<KP>, (unsigned)((own.hchunks.n + 3) / 4), BLOCK, 0, (uint64_t)own.hchunks.n,
+                   (const Job *)own.hchunks.p, (const uint32_t *)own.ycol.p, (const float *)nullptr, (const float *)h.Q1,
+                   (uint64_t)h.partner->R, (float *)hotG_.p, (float *)hotP_.p, (const float *)nullptr,
+                   (const float *)nullptr, 0.0f);
+            done = true;
+          }
+        }
+        if (!done)
+          launch(k_hot_gram<real, KP>, (unsigned)own.hchunks.n, BLOCK, 0, (const Job *)own.hchunks.p,
+                 (const uint32_t *)own.ycol.p, (const real *)nullptr, (const real *)h.Q1, hotG_.p, hotP_.p);
+        if (own.hsums.n)
+          launch(k_hot_slot_sum<real, KP>, (unsigned)own.hsums.n, BLOCK, 0, (const Job *)own.hsums.p,
+                 (const real *)hotP_.p, hotG_.p);
+      }, 2.0 * own.hpos * KP * KP);
+    });
+  }
+
   // Gram chunks of a one-node-per-row field (build_csc's column order): each
   // column in chunks of at most cgram_rows rows (one LDS stage: larger
   // OCFFM_CGRAM_CHUNK values are capped there); empty columns get one empty
@@ -1972,7 +2103,104 @@ template <typename real> class Problem final : public ProblemBase {
 
   // Side half whose CG steps run on per-column Grams (several ranks: each
   // builds its partial Grams, and every CG step all-reduces G_c p_c).
-  bool cgram(const HalfCtx &h) const { return !h.cross && h.F->gchunks.n; }
+  bool cgram(const HalfCtx &h) const { return h.cross ? ccg_now_ : h.F->gchunks.n > 0; }
+
+  // ---- per-column cross Grams.  A cross half over a one-node-per-row field
+  // has, per column c (rows i with idx_i = c, value x_i),
+  //   (X^T h)_c = sum_i x_i h_i = C_c p_c,
+  //   C_c = (1 - w) sum_i x_i^2 sum_{j in Omega_i} q_j q_j^T + w (sum_i x_i^2) QTQ
+  // (hs_cross, ffm.cpp:706-742, summed per column): with few columns (an
+  // artist or genre field) a CG step is D k x k products (k_hv_cgram)
+  // instead of a pass gathering every positive's partner row plus a
+  // feature pass.  Built once per half (the partner table is fixed there)
+  // where the previous epoch's CG count says it pays (OCFFM_CCG: 0 off,
+  // 1 when the half ran >= 3 steps, 2 always).
+  bool ccg_eligible(const HalfCtx &h) const {
+    return ccg_mode_ != 0 && h.cross && h.F->one && !h.F->idlike && h.own->npos > 0 && h.own->R > 0 &&
+           (ccg_mode_ == 2 || kp_ == 32 || kp_ == 64) &&
+           (double)h.D * kp_ * kp_ * sizeof(real) <= 64.0 * (1 << 20);
+  }
+  void ccg_setup(const HalfCtx &h) {
+    DevField<real> &F = *h.F;
+    DevSide<real> &own = *h.own;
+    if (F.ccg_ready) return;
+    auto down = [&](auto &buf, size_t n) {
+      std::vector<typename std::remove_pointer<decltype(buf.p)>::type> v(n);
+      if (n) HIPCHK(hipMemcpy(v.data(), buf.p, n * sizeof(v[0]), hipMemcpyDeviceToHost));
+      return v;
+    };
+    // the field's row CSC: crow/cval in column order; column boundaries from
+    // the rows' one node each (xidx)
+    const auto xidx = down(F.xidx, own.R);
+    const auto crow = down(F.crow, F.crow.n);
+    const auto cval = down(F.cval, F.cval.n);
+    const auto yp = down(own.yptr, own.R + 1);
+    const auto yc = down(own.ycol, own.npos);
+    std::vector<uint32_t> pos;
+    std::vector<real> wt;
+    pos.reserve(own.npos);
+    wt.reserve(own.npos);
+    std::vector<std::pair<uint64_t, uint64_t>> ranges(F.D, {0, 0});
+    uint64_t e = 0;
+    for (uint64_t c = 0; c < F.D; c++) {
+      const uint64_t b0 = pos.size();
+      for (; e < crow.size() && xidx[crow[e]] == c; e++) {
+        const uint32_t i = crow[e];
+        const real x2 = (real)((1 - w_) * (double)cval[e] * (double)cval[e]);  // (1 - w) x_i^2
+        for (int64_t p = yp[i]; p < yp[i + 1]; p++) {
+          pos.push_back(yc[p]);
+          wt.push_back(x2);
+        }
+      }
+      ranges[c] = {b0, pos.size()};
+    }
+    std::vector<Job> chunks, sums;
+    uint64_t slots = 0;
+    // one chunk per column where the columns alone fill the chip (artist:
+    // 5,000 columns of ~420 positions: no partial slots to sum)
+    gram_chunks(ranges, chunks, sums, slots, F.D >= 2048 ? 1024 : HOT_CHUNK_MAX);
+    F.cpos.upload(pos);
+    F.cw.upload(wt);
+    F.cchunks.upload(chunks);
+    F.csums.upload(sums);
+    F.cslots = slots;
+    F.cnpos = pos.size();
+    if (slots * kp_ * kp_ > ccgP_.n) ccgP_.alloc(slots * kp_ * kp_, false);
+    F.ccg_ready = true;
+  }
+  // C_c of every column for this half (needs qtq_: gradient() sets it)
+  void ccg_build(const HalfCtx &h) {
+    DevField<real> &F = *h.F;
+    ccg_setup(h);
+    if (!F.gram.p || F.gram.n < F.D * kp_ * kp_) F.gram.alloc(F.D * kp_ * kp_, false);
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      const double rs = sizeof(real);
+      const double bytes = (double)F.cnpos * (8 + KP * rs) + (double)F.D * KP * KP * rs * 3 +
+                           (double)F.cslots * KP * KP * rs * 2;
+      prof_launch("ccg_build", bytes, [&] {
+        bool done = false;
+        if constexpr (std::is_same<real, float>::value && (KP == 32 || KP == 64)) {
+          if (!no_mfma_) {
+            launch(k_hot_gram_mfma<KP>, (unsigned)((F.cchunks.n + 3) / 4), BLOCK, 0, (uint64_t)F.cchunks.n,
+                   (const Job *)F.cchunks.p, (const uint32_t *)F.cpos.p, (const float *)F.cw.p,
+                   (const float *)h.Q1, (uint64_t)h.partner->R, (float *)F.gram.p, (float *)ccgP_.p,
+                   (const float *)F.xsq.p, (const float *)qtq_, (float)w_);  // tau folded in
+            done = true;
+          }
+        }
+        if (!done)
+          launch(k_hot_gram<real, KP>, (unsigned)F.cchunks.n, BLOCK, 0, (const Job *)F.cchunks.p,
+                 (const uint32_t *)F.cpos.p, (const real *)F.cw.p, (const real *)h.Q1, F.gram.p, ccgP_.p);
+        if (F.csums.n)
+          launch(k_hot_slot_sum<real, KP>, (unsigned)F.csums.n, BLOCK, 0, (const Job *)F.csums.p,
+                 (const real *)ccgP_.p, F.gram.p);
+        if (!done)
+          launch(k_gram_add_tau<real, KP>, grid_for(F.D * KP * KP, BLOCK, 2048), BLOCK, 0, (uint64_t)F.D, F.gram.p,
+                 (const real *)F.xsq.p, (const real *)qtq_, w_);
+      }, 2.0 * F.cnpos * KP * KP);
+    });
+  }
 
   // Does a side half over a one-node-per-row field (R rows, D columns) pay
   // for its Grams?  Estimated time (us) of a half of `c` CG steps, from the
@@ -1992,6 +2220,10 @@ template <typename real> class Problem final : public ProblemBase {
 
   void col_grams(const HalfCtx &h) {
     if (!cgram(h)) return;
+    if (h.cross) {
+      ccg_build(h);
+      return;
+    }
     DevField<real> &F = *h.F;
     DevSide<real> &other = h.user ? V_ : U_;
     if (!F.gram.p) F.gram.alloc(F.D * kp_ * kp_, false);  // every column is stored by its last chunk
@@ -2205,7 +2437,8 @@ template <typename real> class Problem final : public ProblemBase {
             launch(k_hs_cross_seg<real, KP, ML>, grid_for(own.nseg, 4 * Gm::NSG, hs_blocks_), BLOCK, smem, own.nseg,
                    own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.ycol.p, h.Q1, (uint64_t)h.partner->R,
                    coltau(h) ? (const real *)nullptr : (const real *)qtq_, w_, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
-                   F.segd.p, F.segx.p);
+                   F.segd.p, F.segx.p, hot(h) ? (const uint32_t *)own.hot_seg.p : (const uint32_t *)nullptr,
+                   (const real *)hotG_.p);
           };
           prof_launch("hs_cross_row", bytes, [&] {
             if (lds) go(std::true_type());
@@ -2246,8 +2479,6 @@ template <typename real> class Problem final : public ProblemBase {
     // last verdict has been read and the iterations queued past it are no-ops.
     std::memset(run_host_, 0, sizeof(int) * (MAXCG + 2));
     std::atomic_thread_fence(std::memory_order_seq_cst);
-    gradient(h);
-    col_grams(h);
     // CG with `lookahead_` iterations in flight (see file header): iteration
     // it is enqueued before the host waits for iteration it-L's verdict, so
     // the GPU never waits on the host.  Iterations past the real exit run as
@@ -2281,13 +2512,30 @@ template <typename real> class Problem final : public ProblemBase {
                                                 : 0;
     bool queued = false;
     const size_t pend0 = pending_.size();
-    for (int it = 1; it <= MAXCG && !done && !queued; it++) {
+    int it0 = 1;
+    const int last = key < pred_.size() ? pred_[key] : 0;
+    ccg_now_ = ccg_eligible(h) && (ccg_mode_ == 2 || last >= 3);
+    hot_now_ = last >= hot_steps_;
+    // Graph mode (OCFFM_GRAPH=1, one GPU, no profiling): the half's
+    // gradient, its first `pred` CG steps and the guarded update as one
+    // captured hipGraph, replayed in later epochs (measured).
+    if (graph_on_ && !profiling && !comm_.active() && pred >= 1 && pred < MAXCG) {
+      graph_half(h, which, pred);
+      examine(pred + 1);
+      queued = done;  // stopped by iteration pred: the graph's guarded update ran
+      it0 = pred + 1;
+    } else {
+      gradient(h);
+      col_grams(h);
+      hot_grams(h);
+    }
+    for (int it = it0; it <= MAXCG && !done && !queued; it++) {
       prof_tag_ = it;
       hv_pass(h, it);
       prof_tag_ = 0;
       const int t = it - lookahead_;
       if (t >= 1) examine(t + 1);  // upd(t) decided run[t+1]
-      if (!done && it == pred && it < MAXCG) {
+      if (!done && it == pred && it < MAXCG && it0 == 1) {
         prof_tag_ = -1;
         finish_half(h, &st_.p->run[it + 1]);
         prof_tag_ = 0;
@@ -2306,6 +2554,7 @@ template <typename real> class Problem final : public ProblemBase {
       Pending &e = pending_[q];
       if (e.tag > nr || (e.tag == -1 && !queued)) e.name += ".noop";
     }
+    ccg_now_ = hot_now_ = false;
     cg_log.push_back(nr);
     account_half(h, nr);
     if (hb) {
@@ -2315,6 +2564,75 @@ template <typename real> class Problem final : public ProblemBase {
       std::snprintf(name, sizeof(name), "half(%u,%u)%c", f1, f2, which ? 'H' : 'W');
       pending_.push_back({name, 0.0, hb, he, 0, 0.0});
     }
+  }
+
+  // ---- graph mode: the host state the half's enqueue logic reads and
+  // writes (block-excluded base, segment-sum validity, the CG QTQ pointer,
+  // owned-table staleness); a graph captured from one state is replayed
+  // only from that state, and leaves the host state its capture left.
+  struct HostState {
+    bool excl_on, ys0, ys1, owned_stale, lazy_ok;
+    uint32_t excl_b12;
+    const real *qtq;
+    bool operator<(const HostState &o) const {
+      return std::tie(excl_on, ys0, ys1, owned_stale, lazy_ok, excl_b12, qtq) <
+             std::tie(o.excl_on, o.ys0, o.ys1, o.owned_stale, o.lazy_ok, o.excl_b12, o.qtq);
+    }
+  };
+  HostState host_state() const {
+    return HostState{excl_.on, ysum_ok_[0], ysum_ok_[1], owned_stale_, lazy_ok_, excl_.b12, qtq_};
+  }
+  void set_host_state(const HostState &s) {
+    excl_.on = s.excl_on;
+    excl_.b12 = s.excl_b12;
+    ysum_ok_[0] = s.ys0;
+    ysum_ok_[1] = s.ys1;
+    owned_stale_ = s.owned_stale;
+    qtq_ = s.qtq;
+  }
+  struct GraphEntry {
+    hipGraphExec_t exec = nullptr;
+    HostState post;
+  };
+  std::map<std::tuple<uint32_t, int, int, HostState>, GraphEntry> graphs_;
+  bool graph_on_ = std::getenv("OCFFM_GRAPH") && std::atoi(std::getenv("OCFFM_GRAPH")) != 0;
+  bool capturing_ = false;
+
+  void clear_graphs() {
+    for (auto &g : graphs_) (void)hipGraphExecDestroy(g.second.exec);
+    graphs_.clear();
+  }
+
+  void graph_half(HalfCtx &h, int which, int pred) {
+    const auto key = std::make_tuple(h.b12, which, pred, host_state());
+    auto itg = graphs_.find(key);
+    if (itg == graphs_.end()) {
+      HIPCHK(hipStreamBeginCapture(stream_, hipStreamCaptureModeRelaxed));
+      capturing_ = true;
+      try {
+        gradient(h);
+        col_grams(h);
+        hot_grams(h);
+        for (int it = 1; it <= pred; it++) hv_pass(h, it);
+        finish_half(h, &st_.p->run[pred + 1]);
+      } catch (...) {
+        capturing_ = false;
+        hipGraph_t g = nullptr;
+        (void)hipStreamEndCapture(stream_, &g);
+        if (g) (void)hipGraphDestroy(g);
+        throw;
+      }
+      capturing_ = false;
+      hipGraph_t g = nullptr;
+      HIPCHK(hipStreamEndCapture(stream_, &g));
+      GraphEntry e;
+      HIPCHK(hipGraphInstantiate(&e.exec, g, nullptr, nullptr, 0));
+      HIPCHK(hipGraphDestroy(g));
+      e.post = host_state();
+      itg = graphs_.emplace(key, e).first;
+    }
+    set_host_state(itg->second.post);
+    HIPCHK(hipGraphLaunch(itg->second.exec, stream_));
   }
 
   // The end of a half: apply S (W += S, the last pending S += alpha p) and
@@ -2452,6 +2770,19 @@ template <typename real> class Problem final : public ProblemBase {
   }
   DevBuf<real> ysum_;
   void ysum_dirty() { ysum_ok_[0] = ysum_ok_[1] = false; }
+  // hot rows: positives per row from which a cross half reads a per-row
+  // Gram (OCFFM_HOT, default 2 KP; 0: off), the Grams and partial slots
+  uint64_t hot_min_ = 0;
+  DevBuf<real> hotG_, hotP_;
+  int hot_steps_ = 6;
+  bool hot_now_ = false;
+  // default: on where the build runs on MFMA (fp32, KP 32 / 64); the fp64
+  // VALU build measured slower than the steps it saves
+  int ccg_mode_ = std::getenv("OCFFM_CCG") ? std::atoi(std::getenv("OCFFM_CCG"))
+                  : (std::is_same<real, float>::value && std::getenv("OCFFM_NO_MFMA") == nullptr) ? 1
+                                                                                                    : 0;
+  bool ccg_now_ = false;  // this cross half's CG steps run on per-column Grams
+  DevBuf<real> ccgP_;     // their partial slots
   // OCFFM_SPEC_FIXED=n (tests): predict n for every half (hits and misses of every kind)
   int spec_fixed_ = std::getenv("OCFFM_SPEC_FIXED") ? std::atoi(std::getenv("OCFFM_SPEC_FIXED")) : 0;
   bool fuse_ = true;

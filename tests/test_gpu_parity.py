@@ -100,8 +100,14 @@ def test_init_state(tiny):
     assert rel(g.get("t"), o.get("t")) <= 1e-12
 
 
+@pytest.mark.parametrize("hot", ["", "2"])
 @pytest.mark.parametrize("self_side", [True, False])
-def test_gradient_and_hv_kernels(self_side):
+def test_gradient_and_hv_kernels(self_side, hot, monkeypatch):
+    """Every half's gradient and Hessian-vector product (fp64) against the
+    oracle.  OCFFM_HOT=2: every cross-half row with >= 2 positives reads a
+    per-row Gram of its partner rows (k_hot_gram) instead of gathering them."""
+    if hot:
+        monkeypatch.setenv("OCFFM_HOT", hot)
     ds = synth.general(seed=5, m=60, n=40, fu=2, fv=2, k=5, nnz_user=2, mean_pos=3.0, vals="real")
     o, g = pair(ds, self_side=self_side, with_test=False)
     rng = np.random.default_rng(0)
@@ -139,7 +145,9 @@ KK_RC = dict(seed=3, m=1500, n=4000, mean=20.0, name="kk_rc")  # ~24 % heavy pos
 
 
 @pytest.mark.parametrize("env", [{}, {"OCFFM_NO_MFMA": "1"}, {"OCFFM_CGRAM": "2"},
-                                 {"OCFFM_CGRAM": "2", "OCFFM_NO_MFMA": "1"}, {"OCFFM_TPRE": "1"}])
+                                 {"OCFFM_CGRAM": "2", "OCFFM_NO_MFMA": "1"}, {"OCFFM_TPRE": "1"},
+                                 {"OCFFM_HOT": "0"}, {"OCFFM_HOT": "2"}, {"OCFFM_HOT": "2", "OCFFM_NO_MFMA": "1"},
+                                 {"OCFFM_CCG": "2"}, {"OCFFM_CCG": "2", "OCFFM_NO_MFMA": "1"}])
 def test_gradient_and_hv_fp32_k32(monkeypatch, env):
     """fp32 at k = 32 (the perf build: the cross halves' k x k Grams on MFMA,
     kernels.hpp k_gram_mfma32; OCFFM_CGRAM=2: every side half of a
@@ -289,14 +297,20 @@ def test_cfg5_shape_fp64():
     np.testing.assert_allclose(vg["ndcg"], vo["ndcg"], atol=1e-12)
 
 
+@pytest.mark.parametrize("hot", ["", "2"])
 @pytest.mark.parametrize("k,fu", [(64, 39), (32, 20)])
-def test_cfg5_shape_fp32_mfma(k, fu):
+def test_cfg5_shape_fp32_mfma(k, fu, hot, monkeypatch):
     """The fp32 perf path at config-5 structure: the cross halves' T_i on MFMA
     ahead of the gradient pass (k_rows_T<KP>: the C Grams exceed 64 KB of
     LDS) and, at k = 64, the C cross Grams on MFMA (k_gram_mfma64), checked
     per half against the fp64 oracle (gradient and Hessian-vector within
     1e-4 of their largest entry) on 2,000 rows (several row chunks per
-    block of both kernels, ragged tails)."""
+    block of both kernels, ragged tails).  OCFFM_HOT=2: the item halves'
+    popular items (and every row with >= 2 positives) on per-row Grams built
+    on MFMA (k_hot_gram_mfma, KP = 32 / 64; multi-chunk items summed in slot
+    order)."""
+    if hot:
+        monkeypatch.setenv("OCFFM_HOT", hot)
     ds = _cfg5_small(m=2003, n=301, k=k, fu=fu, seed=43, test_rows=0)
     o, g = pair(ds, precision=ocffm.FP32, self_side=False, k=k, with_test=False)
     rng = np.random.default_rng(5)
@@ -339,15 +353,20 @@ HEAVY = dict(seed=13, m=1500, n=300, fu=2, fv=2, k=8, d_user=[1500, 3], d_item=[
              mean_pos=12.0, vals="real")
 
 
-@pytest.mark.parametrize("cgram", ["2", "0"])
+@pytest.mark.parametrize("cgram", ["2", "0", "ccg"])
 @pytest.mark.parametrize("precision", [ocffm.FP64, ocffm.FP32])
 def test_heavy_columns(precision, cgram, monkeypatch):
     """Low-cardinality fields: columns with hundreds of rows go through the
     feature pass as several wave-chunks summed by the last to arrive
     (kernels.hpp: Job), in both the row and the segment CSC.  With
     OCFFM_CGRAM=2 the side halves of the one-node fields run on per-column
-    Grams built from several chunks each (k_col_gram: ordered partial slots)."""
-    monkeypatch.setenv("OCFFM_CGRAM", cgram)
+    Grams built from several chunks each (k_col_gram: ordered partial slots).
+    "ccg": the cross halves over the one-node item fields on per-column cross
+    Grams (OCFFM_CCG=2; real-valued x: weights x^2, multi-chunk columns)."""
+    if cgram == "ccg":
+        monkeypatch.setenv("OCFFM_CCG", "2")
+    else:
+        monkeypatch.setenv("OCFFM_CGRAM", cgram)
     ds = synth.general(**HEAVY)
     o, g = pair(ds, precision=precision, with_test=False)
     for e in (1, 2):
@@ -436,7 +455,8 @@ def test_speculative_update_bit_identical(monkeypatch):
                                  {"OCFFM_SEG_LEN": "2"}, {"OCFFM_CGRAM": "0"},
                                  {"OCFFM_NO_FOLD": "1"}, {"OCFFM_LAZY_BASE": "0"},
                                  {"OCFFM_SPEC_FIXED": "1"}, {"OCFFM_SPEC_FIXED": "2"}, {"OCFFM_SPEC": "0"},
-                                 {"OCFFM_YSUM": "0"}, {"OCFFM_YTVIA": "0"}])
+                                 {"OCFFM_YSUM": "0"}, {"OCFFM_YTVIA": "0"}, {"OCFFM_HOT": "0"},
+                                 {"OCFFM_HOT": "3"}, {"OCFFM_EXACT_R2": "1"}, {"OCFFM_CCG": "0"}, {"OCFFM_CCG": "2"}])
 def test_execution_variants_fp64(kk_small, monkeypatch, env):
     """Schedule knobs (id-field row fusion, segment length, CG look-ahead)
     change the kernels that run, never the result."""

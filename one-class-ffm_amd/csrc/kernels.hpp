@@ -54,7 +54,10 @@ constexpr int BLOCK = 256;   // 4 waves
 #define OCFFM_HS_OCC 1
 #endif
 #ifndef OCFFM_GD_GB
-#define OCFFM_GD_GB 8  // partner-row gathers per round in k_gd_cross_seg
+#define OCFFM_GD_GB 8  // partner-row gathers per round in k_gd_cross_seg (entering a block: two gathers each)
+#endif
+#ifndef OCFFM_GD_GB_IN
+#define OCFFM_GD_GB_IN OCFFM_GD_GB  // the same in the passes with one gather per positive
 #endif
 #ifndef OCFFM_HS_GB
 #define OCFFM_HS_GB 32  // partner-row gathers per round in k_hs_cross_seg
@@ -908,7 +911,7 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
                                                         const real *__restrict__ Tpre,
                                                         const real *__restrict__ ytv) {
   using G = Geo<real, KP>;
-  using PP = PosPass<real, KP, OCFFM_GD_GB>;
+  using PP = PosPass<real, KP, BM == BM_ENTER ? OCFFM_GD_GB : OCFFM_GD_GB_IN>;
   // TP: T_i precomputed by k_rows_T (one row load; no M in LDS)
   // ytv (BM_IN): the stored value is read from the other orientation through
   // perm (ytv[perm[q]]), so the entering pass of the block needs no refresh

@@ -10,7 +10,7 @@ mkdir -p $out
 : > $out/ab.txt
 for r in $(seq 1 $rounds); do
   for cfg in "$@"; do
-    env $cfg timeout -k 10 120 python bench.py --steps 10 --warmup 2 --cpu-baseline off --sgd off > $out/ab.json 2> $out/ab.err
+    env $cfg timeout -k 10 120 python bench.py --steps 10 --warmup 2 --cpu-baseline off --modes off --sgd off > $out/ab.json 2> $out/ab.err
     python - "$cfg" >> $out/ab.txt <<'PY'
 import json, sys
 d = json.loads(open("gpurun_out/ab.json").read().strip().splitlines()[-1])

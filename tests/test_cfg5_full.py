@@ -1,8 +1,8 @@
 """BASELINE configs[4] at full per-GPU size (SURVEY §8d restated: one GPU's
-row shard of the 100 M-row run): --ns, 39 user fields of 250,000 features,
-1 item field (250,000 items), k = 64, 2,000,000 rows, fp32.  The 39 user-side
-P caches alone are 39 x 2 M x 64 x 4 B = 20 GB, so every pass streams from
-HBM, not from the 256 MB Infinity Cache.
+row shard of the 100 M-row, 8-GPU run): --ns, 39 user fields of 250,000
+features, 1 item field (250,000 items), k = 64, 12,500,000 rows, fp32.  The
+39 user-side P caches alone are 39 x 12.5 M x 64 x 4 B = 125 GB, so every pass
+streams from HBM, not from the 256 MB Infinity Cache.
 
 The fp64 oracle cannot run this size in a test, so the checks are
 size-independent properties of one epoch (the structure itself is
@@ -14,6 +14,8 @@ parity-tested at small size in test_gpu_parity.py::test_cfg5_shape_*):
   * validation over 2,000 test rows x 250,000 items gives a finite loss and
     p@k / nDCG@k in [0, 1].
 """
+import time
+
 import numpy as np
 import pytest
 
@@ -24,8 +26,10 @@ import synth
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.timeout(400)
 def test_cfg5_full_size_properties():
-    m, fu, k = 2_000_000, 39, 64
+    m, fu, k = 12_500_000, 39, 64
+    t0 = time.perf_counter()
     ds = synth.cfg5(m=m, test_rows=2000)
     g = ocffm.problem_from_dataset(ds, precision=ocffm.FP32, self_side=False, k=k)
     ocffm.srand(1)
@@ -51,3 +55,4 @@ def test_cfg5_full_size_properties():
     assert np.all((met["prec"] >= 0) & (met["prec"] <= 1))
     assert np.all((met["ndcg"] >= 0) & (met["ndcg"] <= 1))
     g.close()
+    print(f"config-5 shard of {m} rows: {time.perf_counter() - t0:.1f} s for data, one epoch and the checks")

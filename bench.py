@@ -326,10 +326,12 @@ def cfg5_mode(args):
         ds = synth.cfg5(m=rows)
         gen = time.perf_counter() - t0
         steps = max(1, min(args.steps, args.cfg5_steps))
-        r = run_newton(ds, ocffm.FP32, steps, 1, k=64, self_side=False, pmc_tag="cfg5_")
+        # two warm-up epochs: epoch 2 is the shard's slowest (most CG steps)
+        # and the halves' column-Gram choice follows the previous epoch's counts
+        r = run_newton(ds, ocffm.FP32, steps, 2, k=64, self_side=False, pmc_tag="cfg5_")
         return {"metric": "train instances/sec, config-5 shard (39+1 fields, 250k feats/field, k=64, --ns)",
                 "value": round(rows * steps / r["dt"], 1), "unit": "instances/s", "dtype": "f32",
-                "steps": steps, "ms_per_step": round(r["dt"] / steps * 1e3, 3),
+                "steps": steps, "warmup": 2, "ms_per_step": round(r["dt"] / steps * 1e3, 3),
                 "config": {"workload": "BASELINE configs[4] restated (SURVEY §8d): one GPU's row shard "
                                        "(100 M rows / 8 GPUs)" if rows == CFG5_ROWS else
                                        f"BASELINE configs[4] structure, {rows} rows (not the 8-GPU shard)",

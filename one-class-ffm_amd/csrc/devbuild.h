@@ -109,14 +109,16 @@ class Builder {
 
   void sync() { HIPCHK(hipStreamSynchronize(s_)); }
 
- private:
-  void incl_scan(const int64_t *in, int64_t *out, uint64_t n);
   // stable sort of (key, position) pairs: vout[q] = input position of the
   // q-th smallest key (ties in input order)
   void sort_positions(const uint32_t *kin, uint32_t *kout, uint32_t *vout, uint64_t n, uint64_t maxkey);
+  // out[p] = the row of position p of a CSR pointer (R + 1)
   void rowid(const int64_t *ptr, uint64_t R, uint32_t *out);
   // CSR pointer (D + 1) of sorted keys
   void bounds(const uint32_t *sorted, uint64_t n, uint64_t D, int64_t *ptr);
+
+ private:
+  void incl_scan(const int64_t *in, int64_t *out, uint64_t n);
   // scratch buffers reused across calls (grown, never shrunk; a larger one
   // replaces the old only once the stream has drained)
   template <class T> T *grow(DevBuf<T> &b, uint64_t n) {

@@ -259,12 +259,15 @@ __device__ __forceinline__ vec_t<real> sg_vecmat(const vec_t<real> &x, const rea
 // The same product as a rolled loop (a lane-index shuffle per component, a
 // few rows of M in flight): for a path that runs rarely inside a kernel
 // whose register budget belongs to another path (k_hs_cross_seg's hot rows).
-template <typename real, int KP>
+// UNR: iterations in flight (VE rows of M each); 0 = the default for the
+// hot rows of k_hs_cross_seg (2 at KP <= 32, else 1: that kernel's 4
+// waves/SIMD register budget)
+template <typename real, int KP, int UNR_ = 0>
 __device__ __forceinline__ vec_t<real> sg_vecmat_rolled(const vec_t<real> &x, const real *M, int li) {
   using G = Geo<real, KP>;
   const int base = (int)(threadIdx.x & 63) & ~(G::LPR - 1);
   vec_t<real> t = vzero<real>();
-  constexpr int UNR = KP <= 32 ? 2 : 1;  // loads in flight vs the host kernel's 4 waves/SIMD budget
+  constexpr int UNR = UNR_ > 0 ? UNR_ : (KP <= 32 ? 2 : 1);
 #pragma unroll UNR
   for (int l = 0; l < G::LPR; l++) {
 #pragma unroll
@@ -1540,14 +1543,38 @@ __global__ __launch_bounds__(BLOCK) void k_gram_add_tau(uint64_t D, real *__rest
     G[t] += (real)(w * (double)xsq[t / KK]) * QTQ[t % KK];
 }
 
+// Per-column cross Grams, their positions in column order (set up once per
+// field): key[p] = the column of position p's row (a one-node field),
+// then (after a stable sort of the keys) cpos[t] = partner row of the t-th
+// position, cw[t] = (1 - w) x^2 of its row.
+static __global__ __launch_bounds__(BLOCK) void k_pos_colkey(uint64_t P, const uint32_t *__restrict__ rid,
+                                                      const uint32_t *__restrict__ xidx, uint32_t *__restrict__ key) {
+  const uint64_t p = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (p < P) key[p] = xidx[rid[p]];
+}
+template <typename real>
+__global__ __launch_bounds__(BLOCK) void k_ccg_gather(uint64_t P, const uint32_t *__restrict__ perm,
+                                                      const uint32_t *__restrict__ rid, const uint32_t *__restrict__ ycol,
+                                                      const real *__restrict__ xval, double w, uint32_t *__restrict__ cpos,
+                                                      real *__restrict__ cw) {
+  const uint64_t t = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (t >= P) return;
+  const uint32_t p = perm[t];
+  const double x = (double)xval[rid[p]];
+  cpos[t] = ycol[p];
+  cw[t] = (real)((1 - w) * x * x);
+}
+
 // G of a multi-chunk row = its partial slots summed in slot order (sums:
-// Job{col = Gram slot, nparts, slot = first partial slot}); one block per row.
+// Job{col = Gram slot, nparts, slot = first partial slot}); blockIdx.x: the
+// Gram, blockIdx.y: a range of BLOCK of its elements (a column of a few
+// hundred chunks keeps one element per thread in flight).
 template <typename real, int KP>
 __global__ __launch_bounds__(BLOCK) void k_hot_slot_sum(const Job *__restrict__ sums, const real *__restrict__ gpart,
                                                         real *__restrict__ G) {
   constexpr int KK = KP * KP, GB = 8;
   const Job jb = sums[blockIdx.x];
-  for (int t = threadIdx.x; t < KK; t += BLOCK) {
+  for (int t = blockIdx.y * BLOCK + threadIdx.x; t < KK; t += gridDim.y * BLOCK) {
     const real *src = gpart + (size_t)jb.slot * KK + t;
     real acc = src[0];
     for (uint32_t q0 = 1; q0 < jb.nparts; q0 += GB) {
@@ -1580,7 +1607,11 @@ __global__ __launch_bounds__(BLOCK) void k_hv_cgram(uint64_t D, const real *__re
     const FinOps<real> ops = fin_load<real, KP, 1>(f, (uint32_t)c, upd, li);
     vec_t<real> pt = ops.w_or_p;
     if (upd) pt = (ops.r - vsplat<real>(alpha) * ops.hp) + vsplat<real>(beta) * ops.w_or_p;
-    const vec_t<real> s = sg_vecmat<real, KP>(pt, G + c * KP * KP, li);
+    // KP >= 64: the product rolled (16 rows of G in flight; unrolled it took
+    // 624 registers at KP = 64, one wave per SIMD with spills)
+    vec_t<real> s;
+    if constexpr (KP >= 64) s = sg_vecmat_rolled<real, KP, 4>(pt, G + c * KP * KP, li);
+    else s = sg_vecmat<real, KP>(pt, G + c * KP * KP, li);
     if constexpr (MODE == 2) vst<real>(f.acc + c * KP + li * Gm::VE, s);
     else col_finalize<real, KP, 1>(f, (uint32_t)c, s, alpha, beta, upd, li, dsum, ops);
   }

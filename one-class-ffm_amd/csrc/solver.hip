@@ -436,6 +436,11 @@ template <typename real> class Problem final : public ProblemBase {
       if (nh) hotG_.alloc(nh * kp_ * kp_, false);
       if (ns) hotP_.alloc(ns * kp_ * kp_, false);
     }
+    // per-column cross Grams: every eligible field's positions in column
+    // order, set up here (device sort) rather than inside an epoch
+    for (DevSide<real> *sd : {&U_, &V_})
+      for (auto &F : sd->F)
+        if (ccg_field(*F, *sd)) ccg_setup(*F, *sd);
     // T pre-pass rows: the larger side that takes the pre-pass (tpre() also
     // bounds R for 32-bit buffer offsets, so test each side on its own)
     uint64_t tR = 0;
@@ -1988,10 +1993,11 @@ template <typename real> class Problem final : public ProblemBase {
   // chunks of a multi-chunk Gram write consecutive partial slots, summed in
   // slot order by k_hot_slot_sum (sums: {gram, nparts, first slot}).
   static void gram_chunks(const std::vector<std::pair<uint64_t, uint64_t>> &ranges, std::vector<Job> &chunks,
-                          std::vector<Job> &sums, uint64_t &slots, uint64_t cmax = HOT_CHUNK_MAX) {
+                          std::vector<Job> &sums, uint64_t &slots, uint64_t cmax = HOT_CHUNK_MAX,
+                          uint64_t npmax = 64) {
     for (uint64_t g = 0; g < ranges.size(); g++) {
       const uint64_t b = ranges[g].first, e = ranges[g].second;
-      const uint64_t np = std::max<uint64_t>(1, std::min<uint64_t>(64, (e - b + cmax - 1) / cmax));
+      const uint64_t np = std::max<uint64_t>(1, std::min<uint64_t>(npmax, (e - b + cmax - 1) / cmax));
       const uint64_t len = (e - b + np - 1) / std::max<uint64_t>(np, 1);
       for (uint64_t q = 0; q < np; q++)
         chunks.push_back(Job{(uint32_t)g, (uint32_t)np, np > 1 ? (uint32_t)(slots + q) : 0u, (uint32_t)q,
@@ -2066,8 +2072,8 @@ template <typename real> class Problem final : public ProblemBase {
           launch(k_hot_gram<real, KP>, (unsigned)own.hchunks.n, BLOCK, 0, (const Job *)own.hchunks.p,
                  (const uint32_t *)own.ycol.p, (const real *)nullptr, (const real *)h.Q1, hotG_.p, hotP_.p);
         if (own.hsums.n)
-          launch(k_hot_slot_sum<real, KP>, (unsigned)own.hsums.n, BLOCK, 0, (const Job *)own.hsums.p,
-                 (const real *)hotP_.p, hotG_.p);
+          launch(k_hot_slot_sum<real, KP>, dim3((unsigned)own.hsums.n, (KP * KP + BLOCK - 1) / BLOCK), BLOCK, 0,
+                 (const Job *)own.hsums.p, (const real *)hotP_.p, hotG_.p);
       }, 2.0 * own.hpos * KP * KP);
     });
   }
@@ -2104,6 +2110,7 @@ template <typename real> class Problem final : public ProblemBase {
   // Side half whose CG steps run on per-column Grams (several ranks: each
   // builds its partial Grams, and every CG step all-reduces G_c p_c).
   bool cgram(const HalfCtx &h) const { return h.cross ? ccg_now_ : h.F->gchunks.n > 0; }
+  const real *gram_of(const HalfCtx &h) const { return h.cross ? ccgG_.p : h.F->gram.p; }
 
   // ---- per-column cross Grams.  A cross half over a one-node-per-row field
   // has, per column c (rows i with idx_i = c, value x_i),
@@ -2115,64 +2122,60 @@ template <typename real> class Problem final : public ProblemBase {
   // feature pass.  Built once per half (the partner table is fixed there)
   // where the previous epoch's CG count says it pays (OCFFM_CCG: 0 off,
   // 1 when the half ran >= 3 steps, 2 always).
-  bool ccg_eligible(const HalfCtx &h) const {
-    return ccg_mode_ != 0 && h.cross && h.F->one && !h.F->idlike && h.own->npos > 0 && h.own->R > 0 &&
+  // A field whose cross halves can run on column Grams: one node per row,
+  // not id-like (a column per row: the per-row Gram), columns few enough
+  // that one Gram step reads less than a row pass gathers (D KP <= (P + 2R)
+  // / 2: positives' partner rows plus the h round trip), the Grams within
+  // 8 GB.  The positions in column order are set up once (ccg_setup).
+  bool ccg_field(const DevField<real> &F, const DevSide<real> &own) const {
+    return ccg_mode_ != 0 && C_ > 0 && F.one && !F.idlike && own.npos > 0 && own.R > 0 &&
            (ccg_mode_ == 2 || kp_ == 32 || kp_ == 64) &&
-           (double)h.D * kp_ * kp_ * sizeof(real) <= 64.0 * (1 << 20);
+           (double)F.D * kp_ * kp_ * sizeof(real) <= 8.0 * (1ull << 30) &&
+           (ccg_mode_ == 2 || 2.0 * F.D * kp_ <= (double)own.npos + 2.0 * own.R);
   }
-  void ccg_setup(const HalfCtx &h) {
-    DevField<real> &F = *h.F;
-    DevSide<real> &own = *h.own;
+  bool ccg_eligible(const HalfCtx &h) const { return h.cross && h.F->ccg_ready; }
+  void ccg_setup(DevField<real> &F, DevSide<real> &own) {
     if (F.ccg_ready) return;
-    auto down = [&](auto &buf, size_t n) {
-      std::vector<typename std::remove_pointer<decltype(buf.p)>::type> v(n);
-      if (n) HIPCHK(hipMemcpy(v.data(), buf.p, n * sizeof(v[0]), hipMemcpyDeviceToHost));
-      return v;
-    };
-    // the field's row CSC: crow/cval in column order; column boundaries from
-    // the rows' one node each (xidx)
-    const auto xidx = down(F.xidx, own.R);
-    const auto crow = down(F.crow, F.crow.n);
-    const auto cval = down(F.cval, F.cval.n);
-    const auto yp = down(own.yptr, own.R + 1);
-    const auto yc = down(own.ycol, own.npos);
-    std::vector<uint32_t> pos;
-    std::vector<real> wt;
-    pos.reserve(own.npos);
-    wt.reserve(own.npos);
-    std::vector<std::pair<uint64_t, uint64_t>> ranges(F.D, {0, 0});
-    uint64_t e = 0;
-    for (uint64_t c = 0; c < F.D; c++) {
-      const uint64_t b0 = pos.size();
-      for (; e < crow.size() && xidx[crow[e]] == c; e++) {
-        const uint32_t i = crow[e];
-        const real x2 = (real)((1 - w_) * (double)cval[e] * (double)cval[e]);  // (1 - w) x_i^2
-        for (int64_t p = yp[i]; p < yp[i + 1]; p++) {
-          pos.push_back(yc[p]);
-          wt.push_back(x2);
-        }
-      }
-      ranges[c] = {b0, pos.size()};
-    }
+    const uint64_t P = own.npos;
+    dev::Builder B(stream_);
+    DevBuf<uint32_t> rid, key, kout, perm;
+    rid.alloc(P, false);
+    key.alloc(P, false);
+    kout.alloc(P, false);
+    perm.alloc(P, false);
+    B.rowid(own.yptr.p, own.R, rid.p);  // the row of every position
+    launch(k_pos_colkey, (unsigned)((P + BLOCK - 1) / BLOCK), BLOCK, 0, P, (const uint32_t *)rid.p,
+           (const uint32_t *)F.xidx.p, key.p);
+    B.sort_positions(key.p, kout.p, perm.p, P, F.D);  // stable: rows in order inside a column
+    DevBuf<int64_t> cptr;
+    cptr.alloc(F.D + 1, false);
+    B.bounds(kout.p, P, F.D, cptr.p);
+    F.cpos.alloc(P, false);
+    F.cw.alloc(P, false);
+    launch(k_ccg_gather<real>, (unsigned)((P + BLOCK - 1) / BLOCK), BLOCK, 0, P, (const uint32_t *)perm.p,
+           (const uint32_t *)rid.p, (const uint32_t *)own.ycol.p, (const real *)F.xval.p, w_, F.cpos.p, F.cw.p);
+    std::vector<int64_t> cp(F.D + 1);
+    HIPCHK(hipMemcpyAsync(cp.data(), cptr.p, cp.size() * sizeof(int64_t), hipMemcpyDeviceToHost, stream_));
+    sync();
+    std::vector<std::pair<uint64_t, uint64_t>> ranges(F.D);
+    for (uint64_t c = 0; c < F.D; c++) ranges[c] = {(uint64_t)cp[c], (uint64_t)cp[c + 1]};
     std::vector<Job> chunks, sums;
     uint64_t slots = 0;
     // one chunk per column where the columns alone fill the chip (artist:
-    // 5,000 columns of ~420 positions: no partial slots to sum)
-    gram_chunks(ranges, chunks, sums, slots, F.D >= 2048 ? 1024 : HOT_CHUNK_MAX);
-    F.cpos.upload(pos);
-    F.cw.upload(wt);
+    // 5,000 columns of ~420 positions: no partial slots to sum); a Pareto
+    // head column (millions of positions) in up to 256 chunks
+    gram_chunks(ranges, chunks, sums, slots, F.D >= 2048 ? 1024 : HOT_CHUNK_MAX, 256);
     F.cchunks.upload(chunks);
     F.csums.upload(sums);
     F.cslots = slots;
-    F.cnpos = pos.size();
+    F.cnpos = P;
+    if (F.D * kp_ * kp_ > ccgG_.n) ccgG_.alloc(F.D * kp_ * kp_, false);
     if (slots * kp_ * kp_ > ccgP_.n) ccgP_.alloc(slots * kp_ * kp_, false);
     F.ccg_ready = true;
   }
   // C_c of every column for this half (needs qtq_: gradient() sets it)
   void ccg_build(const HalfCtx &h) {
     DevField<real> &F = *h.F;
-    ccg_setup(h);
-    if (!F.gram.p || F.gram.n < F.D * kp_ * kp_) F.gram.alloc(F.D * kp_ * kp_, false);
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
       const double rs = sizeof(real);
@@ -2184,19 +2187,19 @@ template <typename real> class Problem final : public ProblemBase {
           if (!no_mfma_) {
             launch(k_hot_gram_mfma<KP>, (unsigned)((F.cchunks.n + 3) / 4), BLOCK, 0, (uint64_t)F.cchunks.n,
                    (const Job *)F.cchunks.p, (const uint32_t *)F.cpos.p, (const float *)F.cw.p,
-                   (const float *)h.Q1, (uint64_t)h.partner->R, (float *)F.gram.p, (float *)ccgP_.p,
+                   (const float *)h.Q1, (uint64_t)h.partner->R, (float *)ccgG_.p, (float *)ccgP_.p,
                    (const float *)F.xsq.p, (const float *)qtq_, (float)w_);  // tau folded in
             done = true;
           }
         }
         if (!done)
           launch(k_hot_gram<real, KP>, (unsigned)F.cchunks.n, BLOCK, 0, (const Job *)F.cchunks.p,
-                 (const uint32_t *)F.cpos.p, (const real *)F.cw.p, (const real *)h.Q1, F.gram.p, ccgP_.p);
+                 (const uint32_t *)F.cpos.p, (const real *)F.cw.p, (const real *)h.Q1, ccgG_.p, ccgP_.p);
         if (F.csums.n)
-          launch(k_hot_slot_sum<real, KP>, (unsigned)F.csums.n, BLOCK, 0, (const Job *)F.csums.p,
-                 (const real *)ccgP_.p, F.gram.p);
+          launch(k_hot_slot_sum<real, KP>, dim3((unsigned)F.csums.n, (KP * KP + BLOCK - 1) / BLOCK), BLOCK, 0,
+                 (const Job *)F.csums.p, (const real *)ccgP_.p, ccgG_.p);
         if (!done)
-          launch(k_gram_add_tau<real, KP>, grid_for(F.D * KP * KP, BLOCK, 2048), BLOCK, 0, (uint64_t)F.D, F.gram.p,
+          launch(k_gram_add_tau<real, KP>, grid_for(F.D * KP * KP, BLOCK, 2048), BLOCK, 0, (uint64_t)F.D, ccgG_.p,
                  (const real *)F.xsq.p, (const real *)qtq_, w_);
       }, 2.0 * F.cnpos * KP * KP);
     });
@@ -2402,14 +2405,12 @@ template <typename real> class Problem final : public ProblemBase {
         const Fin<real> fin = make_fin(h, it);
         if (!comm_.active() || repl(h)) {
           prof_launch("hv_cgram", (double)h.D * KP * KP * rs + (double)h.D * KP * rs * (it > 1 ? 9 : 4), [&] {
-            launch(k_hv_cgram<real, KP>, grid_for(h.D, 4 * Gm::NSG, 1024), BLOCK, 0, (uint64_t)h.D,
-                   (const real *)h.F->gram.p, fin);
+            launch(k_hv_cgram<real, KP>, grid_for(h.D, 4 * Gm::NSG, 1024), BLOCK, 0, (uint64_t)h.D, gram_of(h), fin);
           });
           return;
         }
         prof_launch("hv_cgram", (double)h.D * KP * KP * rs + (double)h.D * KP * rs * 4, [&] {
-          launch(k_hv_cgram<real, KP, 2>, grid_for(h.D, 4 * Gm::NSG, 1024), BLOCK, 0, (uint64_t)h.D,
-                 (const real *)h.F->gram.p, fin);
+          launch(k_hv_cgram<real, KP, 2>, grid_for(h.D, 4 * Gm::NSG, 1024), BLOCK, 0, (uint64_t)h.D, gram_of(h), fin);
         });
         allreduce_dev(acc_.p, h.D * kp_);
         const uint64_t nv = h.D * KP / Gm::VE;
@@ -2782,7 +2783,7 @@ template <typename real> class Problem final : public ProblemBase {
                   : (std::is_same<real, float>::value && std::getenv("OCFFM_NO_MFMA") == nullptr) ? 1
                                                                                                     : 0;
   bool ccg_now_ = false;  // this cross half's CG steps run on per-column Grams
-  DevBuf<real> ccgP_;     // their partial slots
+  DevBuf<real> ccgG_, ccgP_;  // the column Grams of the current half (max D KP^2), their partial slots
   // OCFFM_SPEC_FIXED=n (tests): predict n for every half (hits and misses of every kind)
   int spec_fixed_ = std::getenv("OCFFM_SPEC_FIXED") ? std::atoi(std::getenv("OCFFM_SPEC_FIXED")) : 0;
   bool fuse_ = true;

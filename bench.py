@@ -171,7 +171,13 @@ def run_newton(ds, prec, steps, warmup, k=32, self_side=True, world=1, rank=0, l
                  "launches": d["launches"], "share_of_kernel_time": round(d["total_ms"] / max(1e-9, tot_ms), 3),
                  "epoch_alg_GBps": round(alg / dt / 1e9, 1), "epoch_alg_bytes": alg / max(1, steps),
                  "families_ms_per_epoch": {kk: round(v["total_ms"] / steps, 3) for kk, v in
-                                           sorted(fams.items(), key=lambda kv: -kv[1]["total_ms"])[:6]}})
+                                           sorted(fams.items(), key=lambda kv: -kv[1]["total_ms"])[:6]},
+                 # the same six families' own rates: algorithmic GB/s per launch (and
+                 # TFLOP/s for the MFMA families) against the same peaks
+                 "families_frac": {kk: round(v["alg_bytes"] / max(1e-12, v["total_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                   if v.get("alg_flops", 0.0) <= RIDGE_FLOP_PER_B * v["alg_bytes"] else
+                                   round(v["alg_flops"] / max(1e-12, v["total_ms"] * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS, 4)
+                                   for kk, v in sorted(fams.items(), key=lambda kv: -kv[1]["total_ms"])[:6]}})
     # HBM bytes per launch of the same kernel family from the committed
     # rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, MI355X guide §HBM).
     pat = f"r*_{pmc_tag}pmc_traffic.json"

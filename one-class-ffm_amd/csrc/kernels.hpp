@@ -1593,9 +1593,12 @@ __global__ __launch_bounds__(BLOCK) void k_hot_slot_sum(const Job *__restrict__ 
 // iteration f.it (formed from r, Hp, p as col_finalize does), s = G_c p_c,
 // then the Hessian-vector finalisation (MODE 1), or s stored into f.acc for
 // the all-reduce of several ranks (MODE 2: the Grams are partials over this
-// rank's positives and rows).  One column per subgroup.
+// rank's positives and rows).  One column per subgroup.  own (an owned
+// field on several ranks): this rank's columns only, whose Grams are whole
+// here; the dot products go to f.dots for the all-reduce (fin_blocks).
 template <typename real, int KP, int MODE = 1>
-__global__ __launch_bounds__(BLOCK) void k_hv_cgram(uint64_t D, const real *__restrict__ G, Fin<real> f) {
+__global__ __launch_bounds__(BLOCK) void k_hv_cgram(uint64_t D, const real *__restrict__ G, Fin<real> f,
+                                                    const uint8_t *__restrict__ own = nullptr) {
   using Gm = Geo<real, KP>;
   if (!f.st->run[f.it]) return;
   const bool upd = f.it > 1;
@@ -1604,6 +1607,7 @@ __global__ __launch_bounds__(BLOCK) void k_hv_cgram(uint64_t D, const real *__re
   const int sg = lane / Gm::LPR, li = lane % Gm::LPR;
   double dsum[3] = {0, 0, 0};
   for (uint64_t c = wave * Gm::NSG + sg; c < D; c += nwaves * Gm::NSG) {
+    if (own && !own[c]) continue;
     const FinOps<real> ops = fin_load<real, KP, 1>(f, (uint32_t)c, upd, li);
     vec_t<real> pt = ops.w_or_p;
     if (upd) pt = (ops.r - vsplat<real>(alpha) * ops.hp) + vsplat<real>(beta) * ops.w_or_p;

@@ -438,9 +438,11 @@ template <typename real> class Problem final : public ProblemBase {
     }
     // per-column cross Grams: every eligible field's positions in column
     // order, set up here (device sort) rather than inside an epoch
+    // (on several ranks: where every rank's shard qualifies, so that the
+    // ranks take the same path and meet in the same all-reduces)
     for (DevSide<real> *sd : {&U_, &V_})
       for (auto &F : sd->F)
-        if (ccg_field(*F, *sd)) ccg_setup(*F, *sd);
+        if (all_ranks(ccg_field(*F, *sd))) ccg_setup(*F, *sd);
     // T pre-pass rows: the larger side that takes the pre-pass (tpre() also
     // bounds R for 32-bit buffer offsets, so test each side on its own)
     uint64_t tR = 0;
@@ -2133,6 +2135,17 @@ template <typename real> class Problem final : public ProblemBase {
            (double)F.D * kp_ * kp_ * sizeof(real) <= 8.0 * (1ull << 30) &&
            (ccg_mode_ == 2 || 2.0 * F.D * kp_ <= (double)own.npos + 2.0 * own.R);
   }
+  // A rank-local condition held on every rank (a vote summed over the ranks).
+  bool all_ranks(bool ok) {
+    if (!comm_.active()) return ok;
+    const double v = ok ? 1.0 : 0.0;
+    HIPCHK(hipMemcpyAsync(dots_.p, &v, sizeof(double), hipMemcpyHostToDevice, stream_));
+    allreduce_dev_d(dots_.p, 1);
+    double sum = 0;
+    HIPCHK(hipMemcpyAsync(&sum, dots_.p, sizeof(double), hipMemcpyDeviceToHost, stream_));
+    sync();
+    return sum == (double)comm_.nranks;
+  }
   bool ccg_eligible(const HalfCtx &h) const { return h.cross && h.F->ccg_ready; }
   void ccg_setup(DevField<real> &F, DevSide<real> &own) {
     if (F.ccg_ready) return;
@@ -2405,12 +2418,23 @@ template <typename real> class Problem final : public ProblemBase {
         const Fin<real> fin = make_fin(h, it);
         if (!comm_.active() || repl(h)) {
           prof_launch("hv_cgram", (double)h.D * KP * KP * rs + (double)h.D * KP * rs * (it > 1 ? 9 : 4), [&] {
-            launch(k_hv_cgram<real, KP>, grid_for(h.D, 4 * Gm::NSG, 1024), BLOCK, 0, (uint64_t)h.D, gram_of(h), fin);
+            launch(k_hv_cgram<real, KP>, grid_for(h.D, 4 * Gm::NSG, 1024), BLOCK, 0, (uint64_t)h.D, gram_of(h), fin,
+                   (const uint8_t *)nullptr);
           });
           return;
         }
+        if (h.F->excl) {  // owned field: this rank's columns are whole here; the dot products meet (feature_pass)
+          prof_launch("hv_cgram", (double)h.D * KP * KP * rs + (double)h.D * KP * rs * (it > 1 ? 9 : 4), [&] {
+            launch(k_hv_cgram<real, KP>, grid_for(h.D, 4 * Gm::NSG, 1024), BLOCK, 0, (uint64_t)h.D, gram_of(h), fin,
+                   (const uint8_t *)h.F->own.p);
+          });
+          allreduce_dev_d(dots_.p, 3);
+          prof_launch("cg_step", 0, [&] { launch(k_cg_step<real, 1>, 1, 64, 0, fin); });
+          return;
+        }
         prof_launch("hv_cgram", (double)h.D * KP * KP * rs + (double)h.D * KP * rs * 4, [&] {
-          launch(k_hv_cgram<real, KP, 2>, grid_for(h.D, 4 * Gm::NSG, 1024), BLOCK, 0, (uint64_t)h.D, gram_of(h), fin);
+          launch(k_hv_cgram<real, KP, 2>, grid_for(h.D, 4 * Gm::NSG, 1024), BLOCK, 0, (uint64_t)h.D, gram_of(h), fin,
+                 (const uint8_t *)nullptr);
         });
         allreduce_dev(acc_.p, h.D * kp_);
         const uint64_t nv = h.D * KP / Gm::VE;

@@ -205,7 +205,8 @@ def _gpu_worker(rank, port, out_dir, world, name="tiny"):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,env", [("tiny", {}), ("owned", {}), ("lowcard", {"OCFFM_CGRAM": "2"}),
                                       ("lowcard", {"OCFFM_CGRAM": "2", "OCFFM_FUSE": "0"}), ("outbrain", {}),
-                                      ("outbrain", {"OCFFM_EXACT_R2": "1"})])
+                                      ("outbrain", {"OCFFM_EXACT_R2": "1"}), ("owned", {"OCFFM_CCG": "2"}),
+                                      ("lowcard", {"OCFFM_CCG": "2", "OCFFM_HOT": "2"})])
 def test_two_ranks_match_one_rank_on_gpu(name, env, monkeypatch):
     import ocffm
     for k, v in env.items():  # inherited by the spawned ranks

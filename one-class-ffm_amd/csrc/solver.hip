@@ -438,11 +438,10 @@ template <typename real> class Problem final : public ProblemBase {
     }
     // per-column cross Grams: every eligible field's positions in column
     // order, set up here (device sort) rather than inside an epoch
-    // (on several ranks: where every rank's shard qualifies, so that the
-    // ranks take the same path and meet in the same all-reduces)
+    // (on several ranks: where every rank's shard qualifies, ccg_field_all)
     for (DevSide<real> *sd : {&U_, &V_})
-      for (auto &F : sd->F)
-        if (all_ranks(ccg_field(*F, *sd))) ccg_setup(*F, *sd);
+      for (uint32_t fi = 0; fi < sd->F.size(); fi++)
+        if (ccg_field_all(*sd->F[fi], *sd, sd == &U_, fi, U)) ccg_setup(*sd->F[fi], *sd);
     // T pre-pass rows: the larger side that takes the pre-pass (tpre() also
     // bounds R for 32-bit buffer offsets, so test each side on its own)
     uint64_t tR = 0;
@@ -2129,22 +2128,46 @@ template <typename real> class Problem final : public ProblemBase {
   // that one Gram step reads less than a row pass gathers (D KP <= (P + 2R)
   // / 2: positives' partner rows plus the h round trip), the Grams within
   // 8 GB.  The positions in column order are set up once (ccg_setup).
-  bool ccg_field(const DevField<real> &F, const DevSide<real> &own) const {
-    return ccg_mode_ != 0 && C_ > 0 && F.one && !F.idlike && own.npos > 0 && own.R > 0 &&
-           (ccg_mode_ == 2 || kp_ == 32 || kp_ == 64) &&
-           (double)F.D * kp_ * kp_ * sizeof(real) <= 8.0 * (1ull << 30) &&
-           (ccg_mode_ == 2 || 2.0 * F.D * kp_ <= (double)own.npos + 2.0 * own.R);
+  bool ccg_pred(uint64_t D, bool one, bool idlike, uint64_t npos, uint64_t R) const {
+    return ccg_mode_ != 0 && C_ > 0 && one && !idlike && npos > 0 && R > 0 &&
+           (ccg_mode_ == 2 || kp_ == 32 || kp_ == 64) && (double)D * kp_ * kp_ * sizeof(real) <= 8.0 * (1ull << 30) &&
+           (ccg_mode_ == 2 || 2.0 * D * kp_ <= (double)npos + 2.0 * R);
   }
-  // A rank-local condition held on every rank (a vote summed over the ranks).
-  bool all_ranks(bool ok) {
-    if (!comm_.active()) return ok;
-    const double v = ok ? 1.0 : 0.0;
-    HIPCHK(hipMemcpyAsync(dots_.p, &v, sizeof(double), hipMemcpyHostToDevice, stream_));
-    allreduce_dev_d(dots_.p, 1);
-    double sum = 0;
-    HIPCHK(hipMemcpyAsync(&sum, dots_.p, sizeof(double), hipMemcpyDeviceToHost, stream_));
-    sync();
-    return sum == (double)comm_.nranks;
+  bool ccg_field(const DevField<real> &F, const DevSide<real> &own) const {
+    return ccg_pred(F.D, F.one, F.idlike, own.npos, own.R);
+  }
+  // On several ranks: the field qualifies on every rank's shard, which each
+  // rank works out from the whole data set it holds (no communication), so
+  // all ranks take the same path and meet in the same all-reduces.  The item
+  // side's rows (all items) are the same on every rank; its positives and
+  // the user side's rows are the shard's.
+  bool ccg_field_all(const DevField<real> &F, const DevSide<real> &own, bool user, uint32_t fi,
+                     const HostData &U) const {
+    if (!ccg_field(F, own)) return false;
+    if (comm_.nranks == 1) return true;
+    const Rows &raw = U.raw;
+    const uint64_t N = (uint64_t)comm_.nranks;
+    for (uint64_t q = 0; q < N; q++) {
+      const uint64_t u0 = U.m * q / N, u1 = U.m * (q + 1) / N;
+      const uint64_t npos = U.yptr[u1] - U.yptr[u0];
+      bool one = F.one, idl = F.idlike;
+      if (user) {
+        one = u1 > u0;
+        std::vector<uint8_t> seen(F.D == u1 - u0 ? F.D : 0, 0);
+        idl = !seen.empty();
+        for (uint64_t i = u0; i < u1 && one; i++) {
+          uint32_t c = 0;
+          uint64_t x = 0;
+          for (uint64_t p = raw.xptr[i]; p < raw.xptr[i + 1]; p++)
+            if (raw.fid[p] == fi) c++, x = raw.idx[p];
+          one = c == 1;
+          if (idl && one) idl = !seen[x], seen[x] = 1;
+        }
+        idl = idl && one;
+      }
+      if (!ccg_pred(F.D, one, idl, npos, user ? u1 - u0 : own.R)) return false;
+    }
+    return true;
   }
   bool ccg_eligible(const HalfCtx &h) const { return h.cross && h.F->ccg_ready; }
   void ccg_setup(DevField<real> &F, DevSide<real> &own) {

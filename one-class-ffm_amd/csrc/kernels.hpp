@@ -65,6 +65,14 @@ constexpr int BLOCK = 256;   // 4 waves
 #ifndef OCFFM_GD_OCC
 #define OCFFM_GD_OCC 1
 #endif
+#ifndef OCFFM_GD_OCC64
+#define OCFFM_GD_OCC64 OCFFM_GD_OCC  // the fp64 build of k_gd_cross_seg
+#endif
+#ifndef OCFFM_GD_GB64
+// fp64: 4 gathers per round (3 / 4 waves per SIMD instead of 2 / 3; the
+// fp64 kkbox epoch's gd_cross_row 206 -> 200 us per launch, 2 is no faster)
+#define OCFFM_GD_GB64 4
+#endif
 constexpr int MAXCG = 20;    // ffm.cpp:761
 constexpr double CG_EPS = 9e-2;  // ffm.cpp:762
 
@@ -900,7 +908,7 @@ __global__ __launch_bounds__(TBLOCK) void k_rows_T(uint64_t R, int C, const floa
 enum { BM_FULL = 0, BM_IN = 1, BM_ENTER = 2 };  // base modes of k_gd_cross_seg
 
 template <typename real, int KP, bool MLDS, int BM, bool TP = false>
-__global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
+__global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_GD_OCC64 : OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                         const uint32_t *__restrict__ ycol,
                                                         real *__restrict__ yt, const real *__restrict__ Q1,
                                                         int C, const real *const *__restrict__ Ptabs,
@@ -914,7 +922,7 @@ __global__ __launch_bounds__(BLOCK, OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t n
                                                         const real *__restrict__ Tpre,
                                                         const real *__restrict__ ytv) {
   using G = Geo<real, KP>;
-  using PP = PosPass<real, KP, BM == BM_ENTER ? OCFFM_GD_GB : OCFFM_GD_GB_IN>;
+  using PP = PosPass<real, KP, sizeof(real) == 8 ? OCFFM_GD_GB64 : (BM == BM_ENTER ? OCFFM_GD_GB : OCFFM_GD_GB_IN)>;
   // TP: T_i precomputed by k_rows_T (one row load; no M in LDS)
   // ytv (BM_IN): the stored value is read from the other orientation through
   // perm (ytv[perm[q]]), so the entering pass of the block needs no refresh

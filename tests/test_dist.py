@@ -257,3 +257,57 @@ def test_rccl_one_rank_matches_single():
             assert np.abs(b.get(what, bl) - ref).max() <= 1e-9 * np.abs(ref).max(), (what, bl)
     ma, mb = a.validate(), b.validate()
     assert abs(ma["loss"] - mb["loss"]) <= 1e-9 * ma["loss"]
+
+
+def _fp32_worker(rank, port, out_dir, world):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import ocffm
+
+    def allreduce(arr):
+        dist.all_reduce(torch.from_numpy(arr))
+
+    ds = synth.kkbox_small()
+    g = ocffm.problem_from_dataset(ds, precision=ocffm.FP32, rank=rank, nranks=world, allreduce=allreduce)
+    ocffm.srand(1)
+    g.init()
+    g.set_profiling(True)
+    for _ in range(4):
+        g.one_epoch()
+    ks = g.kernel_stats()
+    met = g.validate()
+    nb = g.n_blocks()
+    W = [g.get("W", b) for b in range(nb)] + [g.get("H", b) for b in range(nb)]
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), cg=g.cg_log(), loss=met["loss"], ndcg=met["ndcg"],
+             ccg=ks.get("hv_cgram", {}).get("launches", 0), *W)
+    g.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_ranks_fp32_default_path():
+    """The multi-rank line the scale bench runs (fp32, default knobs) on a
+    kkbox-shaped set: the artist / genre item halves go on per-column cross
+    Grams on both ranks (eligibility from the whole data, ccg_field_all), the
+    ranks' replicated tables stay bit-identical, and the run tracks a
+    one-rank run (the all-reduce reorders fp32 sums, so within 1e-3)."""
+    import ocffm
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_fp32_worker, args=(_free_port(), d, WORLD), nprocs=WORLD, join=True)
+        r0 = np.load(os.path.join(d, "r0.npz"))
+        r1 = np.load(os.path.join(d, "r1.npz"))
+    assert int(r0["ccg"]) > 0 and int(r1["ccg"]) > 0
+    np.testing.assert_array_equal(r0["cg"], r1["cg"])
+    nw = len([k for k in r0.files if k.startswith("arr_")])
+    for i in range(nw):
+        np.testing.assert_array_equal(r0[f"arr_{i}"], r1[f"arr_{i}"])
+    ds = synth.kkbox_small()
+    g = ocffm.problem_from_dataset(ds, precision=ocffm.FP32)
+    ocffm.srand(1)
+    g.init()
+    for _ in range(4):
+        g.one_epoch()
+    met = g.validate()
+    g.close()
+    assert abs(float(r0["loss"]) - met["loss"]) <= 1e-3 * met["loss"]
+    np.testing.assert_allclose(r0["ndcg"], met["ndcg"], atol=0.02)

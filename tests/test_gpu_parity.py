@@ -210,8 +210,13 @@ def test_epochs_fp64_tiny(tiny):
     np.testing.assert_array_equal(g.cg_log(), o.cg_log())
 
 
-def test_epochs_fp32_tiny(tiny):
-    o, g = pair(tiny, precision=ocffm.FP32)
+@pytest.mark.parametrize("k", [None, 128])
+def test_epochs_fp32_tiny(tiny, k):
+    """fp32 within 1e-3 of the fp64 oracle (north_star's tolerance); k = 128,
+    the largest k, runs the VALU kernels at 32 lanes of 4 values per row."""
+    kw = {} if k is None else {"k": k}
+    ds = tiny if k is None else synth.tiny(seed=4, m=300)
+    o, g = pair(ds, precision=ocffm.FP32, **kw)
     for e in range(3):
         o.one_epoch()
         g.one_epoch()
@@ -221,18 +226,19 @@ def test_epochs_fp32_tiny(tiny):
     np.testing.assert_allclose(vg["ndcg"], vo["ndcg"], atol=2e-2)
     # objective of the fp32 state, evaluated in fp64 by a second oracle
     f_ref = o.func()
-    o2 = O.Oracle(tiny)
+    o2 = O.Oracle(ds, **kw)
     ocffm.srand(1)
     o2.init()
     f32obj = gpu_objective(o2, g)
     assert abs(f32obj - f_ref) <= 1e-3 * abs(f_ref)
 
 
-@pytest.mark.parametrize("variant", ["ns", "freq", "k5", "k16", "multi_nnz", "k1", "k64", "k100", "sparse",
+@pytest.mark.parametrize("variant", ["ns", "freq", "k5", "k16", "multi_nnz", "k1", "k64", "k100", "k128", "sparse",
                                      "kdd12", "outbrain", "wide_ns"])
 def test_variants_fp64(variant):
-    """Flags and shapes: --ns, --freq, k = 1 / 5 / 16 / 64 / 100 (padded rows of
-    4 .. 128: one to 64 lanes per row), several nodes per field, a sparse
+    """Flags and shapes: --ns, --freq, k = 1 / 5 / 16 / 64 / 100 / 128 (padded
+    rows of 4 .. 128: one to 64 lanes per row; 128 is the largest k the
+    library takes), several nodes per field, a sparse
     set (users and items without positives, empty feature columns), and the
     field structures of BASELINE configs 2, 4 and 5 at test size:
     kdd12-shape (fu=2, fv=4, k=16), outbrain-shape (fu=2, fv=2, k=64, ~1
@@ -252,12 +258,12 @@ def test_variants_fp64(variant):
         ds = synth.general(seed=13, m=120, n=90, fu=2, fv=2, k=4, d_user=[300, 7], d_item=[200, 5], mean_pos=0.7,
                            test_rows=20)
     else:
-        ds = synth.tiny(seed=4, m=300 if variant in ("k64", "k100") else 1000)
-    for name, k in (("k1", 1), ("k5", 5), ("k16", 16), ("k64", 64), ("k100", 100)):
+        ds = synth.tiny(seed=4, m=300 if variant in ("k64", "k100", "k128") else 1000)
+    for name, k in (("k1", 1), ("k5", 5), ("k16", 16), ("k64", 64), ("k100", 100), ("k128", 128)):
         if variant == name:
             kw["k"] = k
     o, g = pair(ds, self_side=variant not in ("ns", "wide_ns"), freq=variant == "freq", **kw)
-    # three epochs.  At k = 64 / 100 block (1,1)'s W half runs into the
+    # three epochs.  At k = 64 / 100 / 128 block (1,1)'s W half runs into the
     # 20-iteration CG cap (ffm.cpp:761) from epoch 2 on this set, and that
     # ill-conditioned solve amplifies any reassociation: the reference's own
     # arithmetic drifts ~1e-6 (k = 64) / ~8e-9 (k = 100) between thread

@@ -14,7 +14,7 @@ Prints, per set and epoch, the max relative state difference (W, H, P, Q of
 every block, a, b, both y~ orientations) of each run against the 1-thread oracle, and whether the CG logs agree.
 
     python tools/fp64_drift.py [epochs] [--json out.json]
-    python tools/fp64_drift.py [epochs] --envelope tests/golden/fp64_envelope.json
+    python tools/fp64_drift.py [epochs] --envelope tests/golden/fp64_envelope.json [--sets a,b]
 
 --envelope (CPU only): the oracle at 2, 3, 4, 6, 8 and 16 threads, twice
 each; per set and epoch the largest drift from the 1-thread run is the
@@ -47,6 +47,7 @@ def names(o):
 SETS = {
     "k64": (lambda: synth.tiny(seed=4, m=300), dict(k=64)),
     "k100": (lambda: synth.tiny(seed=4, m=300), dict(k=100)),
+    "k128": (lambda: synth.tiny(seed=4, m=300), dict(k=128)),
     "wide_ns": (lambda: synth.general(seed=33, m=200, n=40, fu=39, fv=1, k=8, d_user=[20] * 39, d_item=[40],
                                       mean_pos=3.0, test_rows=20, name="wide_ns"), dict(self_side=False)),
     "cfg5_shape": (lambda: synth.general(seed=41, m=300, n=60, fu=39, fv=1, k=64, d_user=[50] * 39, d_item=[60],
@@ -98,9 +99,13 @@ def run_gpu(ds, kw, E, exact):
     return st, cg
 
 
-def envelope(E, path):
+def envelope(E, path, only=None):
     res = {}
+    if only and os.path.exists(path):  # add / refresh some sets of an existing envelope
+        res = json.load(open(path))["sets"]
     for name, (mk, kw) in SETS.items():
+        if only and name not in only:
+            continue
         ds = mk()
         ref, cg1, _ = run_oracle(ds, kw, 1, E)
         env = [0.0] * E
@@ -120,7 +125,8 @@ def envelope(E, path):
 def main():
     E = int(sys.argv[1]) if len(sys.argv) > 1 and not sys.argv[1].startswith("-") else 3
     if "--envelope" in sys.argv:
-        return envelope(E, sys.argv[sys.argv.index("--envelope") + 1])
+        only = sys.argv[sys.argv.index("--sets") + 1].split(",") if "--sets" in sys.argv else None
+        return envelope(E, sys.argv[sys.argv.index("--envelope") + 1], only)
     out = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
     gpu = "--cpu-only" not in sys.argv
     only = sys.argv[sys.argv.index("--sets") + 1].split(",") if "--sets" in sys.argv else list(SETS)

@@ -108,6 +108,69 @@ __global__ __launch_bounds__(256, OCC) void k_gram(uint64_t Rp, int C, const flo
   }
 }
 
+// NS register sets in a ring: set s is consumed NS - 1 sets after its loads
+// were issued (deeper than PIPE 1), U row pairs per set.
+template <int U, int NS, int OCC>
+__global__ __launch_bounds__(256, OCC) void k_gram_deep(uint64_t Rp, int C, const float *const *__restrict__ A,
+                                                        const float *__restrict__ B, const float *__restrict__ wv,
+                                                        float *__restrict__ part, uint64_t nout, uint64_t rows_per_block,
+                                                        unsigned ngroups) {
+  typedef float f16x __attribute__((ext_vector_type(16)));
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int e = lane & 31, hf = lane >> 5;
+  const unsigned grp = blockIdx.x % ngroups, chunk = blockIdx.x / ngroups;
+  const int c0 = (int)(grp * 4 + w);
+  if (c0 >= C) return;
+  f16x acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; t++)
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[t][r] = 0.0f;
+  const BufView ab = buf_view(A[c0], Rp * 256);
+  const BufView bb = buf_view(B, Rp * 256);
+  const uint64_t r0 = (uint64_t)chunk * rows_per_block;
+  const uint64_t r1 = r0 + rows_per_block < Rp ? r0 + rows_per_block : Rp;
+  float bv[NS][U][2], av[NS][U][2];
+  auto load = [&](auto SB, uint64_t j0) {
+    constexpr int sb = decltype(SB)::value;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t jj = j0 + 2 * u + hf;
+      const uint32_t off = jj < r1 ? (uint32_t)(jj * 256 + e * 4) : 0xffffff00u;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        bv[sb][u][h] = bld1<float>(bb, off + h * 128);
+        av[sb][u][h] = bld1<float>(ab, off + h * 128);
+      }
+    }
+  };
+  auto step = [&](auto SB) {
+    constexpr int sb = decltype(SB)::value;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++)
+          acc[mt * 2 + nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[sb][u][mt], bv[sb][u][nt], acc[mt * 2 + nt], 0, 0, 0);
+  };
+  sfor<NS>([&](auto S) { load(S, r0 + decltype(S)::value * 2 * U); });
+  for (uint64_t j0 = r0; j0 < r1; j0 += NS * 2 * U) {
+    sfor<NS>([&](auto S) {
+      step(S);
+      load(S, j0 + (decltype(S)::value + NS) * 2 * U);
+    });
+  }
+  float *out = part + (size_t)chunk * nout;
+#pragma unroll
+  for (int t = 0; t < 4; t++)
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const int m = (t >> 1) * 32 + 8 * (r >> 2) + 4 * hf + (r & 3), n = (t & 1) * 32 + e;
+      out[(size_t)c0 * 4096 + m * 64 + n] = acc[t][r];
+    }
+}
+
 template <class F> float timeit(F &&f, int reps) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
@@ -154,14 +217,14 @@ int main(int argc, char **argv) {
                 flops / us / 1e6 / 157.3, bytes / us / 1e6);
   };
   std::printf("Rp %lu, C %d, blocks %lu (%lu chunks x %u groups), rows/block %lu\n", Rp, C, nbx * gy, nbx, gy, rpb);
-  run("U4 sums pipe0 occ3 (round 2)", k_gram<4, true, 0, 3>);
   run("U4 nosums pipe0 occ3", k_gram<4, false, 0, 3>);
-  run("U4 nosums pipe0 occ2", k_gram<4, false, 0, 2>);
-  run("U4 nosums pipe0 occ4", k_gram<4, false, 0, 4>);
-  run("U2 nosums pipe0 occ4", k_gram<2, false, 0, 4>);
-  run("U8 nosums pipe0 occ2", k_gram<8, false, 0, 2>);
-  run("U2 nosums pipe1 occ4", k_gram<2, false, 1, 4>);
-  run("U6 nosums pipe0 occ3", k_gram<6, false, 0, 3>);
+  run("U4 nosums pipe1 occ3", k_gram<4, false, 1, 3>);
+  run("deep U4 NS3 occ3", k_gram_deep<4, 3, 3>);
+  run("deep U4 NS4 occ3", k_gram_deep<4, 4, 3>);
+  run("deep U2 NS4 occ3", k_gram_deep<2, 4, 3>);
+  run("deep U2 NS6 occ3", k_gram_deep<2, 6, 3>);
+  run("deep U4 NS3 occ2", k_gram_deep<4, 3, 2>);
+  run("deep U2 NS4 occ4", k_gram_deep<2, 4, 4>);
   {  // the library kernel (sums on the matrix cores in the spare wave slot)
     const unsigned gy2 = (C + 1 + 3) / 4;
     const float us = timeit([&] { hipLaunchKernelGGL(k_gram_mfma64, (unsigned)(nbx * gy2), 256, 0, 0, Rp, C,

@@ -1541,6 +1541,74 @@ __global__ __launch_bounds__(BLOCK) void k_hot_gram_mfma(uint64_t nchunks, const
   }
 }
 
+// The fp64 build at KP = 32 on the f64 matrix cores (v_mfma_f64_16x16x4f64,
+// MI355X guide: A lane l = A[m = l%16][k = l/16], B lane l = B[k = l/16][n =
+// l%16], D register r of lane l = element (row l/16 + 4r, column l%16)): four
+// positions are the K dimension, lane l holds w_r q_r[16t + l%16] / q_r[16t +
+// l%16] of position r = l/16 of the group; 32 positions per batch (one
+// coalesced index / weight load), tiles 00, 01 and 11 of the symmetric 32 x 32
+// Gram (10 stored as 01^T), two accumulator sets; the column tau added by the
+// column's first chunk as in k_hot_gram_mfma.
+static __global__ __launch_bounds__(BLOCK) void k_hot_gram_mfma_f64(uint64_t nchunks, const Job *__restrict__ chunks,
+                                                            const uint32_t *__restrict__ ycol,
+                                                            const double *__restrict__ wts,
+                                                            const double *__restrict__ Q1, uint64_t q1rows,
+                                                            double *__restrict__ G, double *__restrict__ gpart,
+                                                            const double *__restrict__ xsq,
+                                                            const double *__restrict__ QTQ, double w) {
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  constexpr int KP = 32, HB = 32, NG = HB / 4, NA = 2;
+  const int lane = threadIdx.x & 63;
+  const uint64_t wv = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+  if (wv >= nchunks) return;
+  const Job jb = chunks[wv];
+  const BufView qb = buf_view(Q1, q1rows * KP * 8);
+  const int c16 = lane & 15, rq = lane >> 4;
+  d4 acc[NA][3];
+#pragma unroll
+  for (int u = 0; u < NA; u++)
+#pragma unroll
+    for (int a = 0; a < 3; a++) acc[u][a] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int64_t b0 = jb.b; b0 < jb.e; b0 += HB) {
+    const int n = (int)(jb.e - b0 < HB ? jb.e - b0 : HB);
+    const uint32_t il = lane < n ? ycol[b0 + lane] : 0u;
+    const double wl = lane < n ? (wts ? wts[b0 + lane] : 1.0) : 0.0;
+    double q0[NG], q1[NG], wg[NG];
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+      const int r = 4 * g + rq;  // positions past n read zero (buffer range check)
+      const uint32_t i = (uint32_t)__shfl((int)il, r, 64);
+      wg[g] = __shfl(wl, r, 64);
+      const uint32_t off = r < n ? i * (uint32_t)(KP * 8) + (uint32_t)c16 * 8u : 0xffffffffu;
+      q0[g] = bld1<double>(qb, off);
+      q1[g] = bld1<double>(qb, r < n ? off + 128u : 0xffffffffu);
+    }
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+      d4(&c)[3] = acc[g % NA];
+      const double a0 = wg[g] * q0[g], a1 = wg[g] * q1[g];
+      c[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, q0[g], c[0], 0, 0, 0);
+      c[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, q1[g], c[1], 0, 0, 0);
+      c[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, q1[g], c[2], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int u = 1; u < NA; u++)
+#pragma unroll
+    for (int a = 0; a < 3; a++) acc[0][a] += acc[u][a];
+  double *out = jb.nparts <= 1 ? G + (size_t)jb.col * KP * KP : gpart + (size_t)jb.slot * KP * KP;
+  const double tw = (xsq && jb.flags == 0) ? w * xsq[jb.col] : 0.0;
+  auto tau = [&](int m, int nn) { return xsq ? tw * QTQ[m * KP + nn] : 0.0; };
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int m = rq + 4 * r;
+    out[m * KP + c16] = acc[0][0][r] + tau(m, c16);
+    out[m * KP + 16 + c16] = acc[0][1][r] + tau(m, 16 + c16);
+    out[(16 + c16) * KP + m] = acc[0][1][r] + tau(16 + c16, m);
+    out[(16 + m) * KP + 16 + c16] = acc[0][2][r] + tau(16 + m, 16 + c16);
+  }
+}
+
 // Per-column cross Grams: C_c += w xsq_c QTQ, the column tau
 // term folded in, so a CG step is C_c p_c alone (k_hv_cgram).
 template <typename real, int KP>

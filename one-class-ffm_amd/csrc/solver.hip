@@ -2129,8 +2129,9 @@ template <typename real> class Problem final : public ProblemBase {
   // / 2: positives' partner rows plus the h round trip), the Grams within
   // 8 GB.  The positions in column order are set up once (ccg_setup).
   bool ccg_pred(uint64_t D, bool one, bool idlike, uint64_t npos, uint64_t R) const {
-    return ccg_mode_ != 0 && C_ > 0 && one && !idlike && npos > 0 && R > 0 &&
-           (ccg_mode_ == 2 || kp_ == 32 || kp_ == 64) && (double)D * kp_ * kp_ * sizeof(real) <= 8.0 * (1ull << 30) &&
+    const bool mfma = kp_ == 32 || (kp_ == 64 && std::is_same<real, float>::value);
+    return ccg_mode_ != 0 && C_ > 0 && one && !idlike && npos > 0 && R > 0 && (ccg_mode_ == 2 || mfma) &&
+           (double)D * kp_ * kp_ * sizeof(real) <= 8.0 * (1ull << 30) &&
            (ccg_mode_ == 2 || 2.0 * D * kp_ <= (double)npos + 2.0 * R);
   }
   bool ccg_field(const DevField<real> &F, const DevSide<real> &own) const {
@@ -2225,6 +2226,15 @@ template <typename real> class Problem final : public ProblemBase {
                    (const Job *)F.cchunks.p, (const uint32_t *)F.cpos.p, (const float *)F.cw.p,
                    (const float *)h.Q1, (uint64_t)h.partner->R, (float *)ccgG_.p, (float *)ccgP_.p,
                    (const float *)F.xsq.p, (const float *)qtq_, (float)w_);  // tau folded in
+            done = true;
+          }
+        }
+        if constexpr (std::is_same<real, double>::value && KP == 32) {
+          if (!no_mfma_) {
+            launch(k_hot_gram_mfma_f64, (unsigned)((F.cchunks.n + 3) / 4), BLOCK, 0, (uint64_t)F.cchunks.n,
+                   (const Job *)F.cchunks.p, (const uint32_t *)F.cpos.p, (const double *)F.cw.p,
+                   (const double *)h.Q1, (uint64_t)h.partner->R, (double *)ccgG_.p, (double *)ccgP_.p,
+                   (const double *)F.xsq.p, (const double *)qtq_, w_);  // tau folded in
             done = true;
           }
         }
@@ -2826,9 +2836,10 @@ template <typename real> class Problem final : public ProblemBase {
   bool hot_now_ = false;
   // default: on where the build runs on MFMA (fp32, KP 32 / 64); the fp64
   // VALU build measured slower than the steps it saves
+  // (default on where the builds run on the matrix cores: fp32 at KP 32 / 64,
+  // fp64 at KP 32, ccg_pred)
   int ccg_mode_ = std::getenv("OCFFM_CCG") ? std::atoi(std::getenv("OCFFM_CCG"))
-                  : (std::is_same<real, float>::value && std::getenv("OCFFM_NO_MFMA") == nullptr) ? 1
-                                                                                                    : 0;
+                  : std::getenv("OCFFM_NO_MFMA") == nullptr ? 1 : 0;
   bool ccg_now_ = false;  // this cross half's CG steps run on per-column Grams
   DevBuf<real> ccgG_, ccgP_;  // the column Grams of the current half (max D KP^2), their partial slots
   // OCFFM_SPEC_FIXED=n (tests): predict n for every half (hits and misses of every kind)

@@ -2534,6 +2534,111 @@ static __global__ __launch_bounds__(BLOCK, 3) void k_gram_mfma64(uint64_t Rp, in
     }
 }
 
+// Cross-half aggregates at KP = 32, fp64, on the f64 matrix cores: M_c =
+// A_c^T B (32 x 32) for every table c < C, oQ = sum_i B_i, bQ = sum_i wv_i
+// B_i and sum wv over block x's row chunk, laid out like k_gram_part's
+// partials (double; k_reduce_parts).  Wave slot c < C owns table c and walks
+// the chunk four rows at a time: v_mfma_f64_16x16x4f64 takes them as the K
+// dimension, lane l supplying A_c[row l/16][16 mt + l%16] and B[row l/16][16
+// nt + l%16] (tiles mt, nt of the 2 x 2 grid; D register r of lane l is
+// element (16 mt + l/16 + 4r, 16 nt + l%16)), two register sets in flight.
+// Wave slot C sums B and wv B on the VALU.
+static __global__ __launch_bounds__(BLOCK) void k_gram_mfma_f64(uint64_t Rp, int C, const double *const *__restrict__ A,
+                                                               const double *__restrict__ B,
+                                                               const double *__restrict__ wv, double *__restrict__ part,
+                                                               uint64_t nout, uint64_t rows_per_block,
+                                                               unsigned ngroups) {
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  constexpr int U = 4;  // groups of four rows per register set
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c16 = lane & 15, rq = lane >> 4;
+  const unsigned grp = blockIdx.x % ngroups, chunk = blockIdx.x / ngroups;
+  const int c0 = (int)(grp * (BLOCK / 64) + w);
+  if (c0 > C) return;  // no barrier below
+  const uint64_t r0 = (uint64_t)chunk * rows_per_block;
+  const uint64_t r1 = r0 + rows_per_block < Rp ? r0 + rows_per_block : Rp;
+  double *out = part + (size_t)chunk * nout;
+  const BufView bb = buf_view(B, Rp * 256);
+  if (c0 == C) {  // the sums slot
+    const BufView wb = buf_view(wv, wv ? Rp * 8 : 0);
+    double cs[2] = {0, 0}, ws[2] = {0, 0}, wt = 0;
+    for (uint64_t j0 = r0; j0 < r1; j0 += 4 * U) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t jj = j0 + 4 * u + rq;
+        const bool ok = jj < r1;
+        const uint32_t off = ok ? (uint32_t)(jj * 256 + c16 * 8) : 0xffffff00u;
+        const double wvi = bld1<double>(wb, ok ? (uint32_t)(jj * 8) : 0xffffff00u);
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          const double b = bld1<double>(bb, off + h * 128);
+          cs[h] += b;
+          ws[h] += wvi * b;
+        }
+        if (c16 == 0) wt += wvi;
+      }
+    }
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) {
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        cs[h] += __shfl_xor(cs[h], o, 64);
+        ws[h] += __shfl_xor(ws[h], o, 64);
+      }
+      wt += __shfl_xor(wt, o, 64);
+    }
+    if (rq == 0) {
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        out[(size_t)C * 1024 + h * 16 + c16] = cs[h];
+        out[(size_t)C * 1024 + 32 + h * 16 + c16] = ws[h];
+      }
+      if (c16 == 0) out[(size_t)C * 1024 + 64] = wt;
+    }
+    return;
+  }
+  const BufView ab = buf_view(A[c0], Rp * 256);
+  d4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; t++) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+  double av[2][U][2], bv[2][U][2];
+  auto load = [&](int sb, uint64_t j0) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t jj = j0 + 4 * u + rq;
+      const uint32_t off = jj < r1 ? (uint32_t)(jj * 256 + c16 * 8) : 0xffffff00u;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        av[sb][u][h] = bld1<double>(ab, off + h * 128);
+        bv[sb][u][h] = bld1<double>(bb, off + h * 128);
+      }
+    }
+  };
+  auto step = [&](int sb) {
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++)
+          acc[mt * 2 + nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[sb][u][mt], bv[sb][u][nt], acc[mt * 2 + nt], 0, 0, 0);
+  };
+  // rows past r1 load zeros (buffer range check), so a trailing round is harmless
+  for (uint64_t j0 = r0; j0 < r1; j0 += 8 * U) {
+    load(0, j0);
+    load(1, j0 + 4 * U);
+    step(0);
+    step(1);
+  }
+#pragma unroll
+  for (int t = 0; t < 4; t++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int m = (t >> 1) * 16 + rq + 4 * r, n = (t & 1) * 16 + c16;
+      out[(size_t)c0 * 1024 + m * 32 + n] = acc[t][r];
+    }
+}
+
 // o in [0, cnt): t = sum_b part[b][off + o]; o < split -> out_real[o] = t,
 // else out_dbl[o - split] = t.  A block owns 16 consecutive outputs
 // (coalesced 128-B reads) and 16 groups of partial rows; groups are combined

@@ -1597,6 +1597,10 @@ template <typename real> class Problem final : public ProblemBase {
       gram64(Rp, L, A, B, wv, M);
       return;
     }
+    if (std::is_same<real, double>::value && kp_ == 32 && L >= 1 && !no_mfma_ && B_ok(Rp) && M && B) {
+      gram_f64(Rp, L, A, B, wv, M);  // fp64, KP = 32: every table in one launch (k_gram_mfma_f64)
+      return;
+    }
     const int TR = kp_ >= 64 ? 16 : 32;
     // tables per launch so the LDS stage fits in 64 KB (MFMA path: its register budget)
     const bool mg = mfma_gram(L) && (uint64_t)Rp * 128 < 0xffffff00ull;  // buffer-load offsets are 32-bit
@@ -1638,6 +1642,29 @@ template <typename real> class Problem final : public ProblemBase {
     prof_launch("aggr_reduce", (double)nbx * cnt * 4, [&] {
       launch(k_reduce_parts<real, float>, (unsigned)((cnt + 15) / 16), BLOCK, 0, nbx, nout, (uint64_t)0, cnt,
              (const float *)gpart64_.p, ng, M, sums_.p);
+    });
+  }
+
+  // KP = 32 fp64 Grams on the f64 matrix cores: the gram64 grid (groups of
+  // four table slots, the last slot the sums, x row chunks), double partials
+  // summed in chunk order (k_reduce_parts).
+  void gram_f64(uint64_t Rp, int L, const real *const *A, const real *B, const real *wv, real *M) {
+    constexpr int TPB = BLOCK / 64;
+    const unsigned gy = (unsigned)((L + 1 + TPB - 1) / TPB);
+    const uint64_t nout = (uint64_t)L * 1024 + 65;
+    uint64_t nbx = std::max<uint64_t>(1, std::min<uint64_t>((Rp + 63) / 64, std::max<uint64_t>(1, gram64_blocks_ / gy)));
+    const uint64_t rpb = ((Rp + nbx - 1) / nbx + 31) / 32 * 32;  // whole rounds of 2 x 4 x 4 rows
+    nbx = std::max<uint64_t>(1, (Rp + rpb - 1) / rpb);
+    if (gpartd_.n < nbx * nout) gpartd_.alloc(nbx * nout, false);
+    const double abytes = (double)Rp * ((L + 1) * 32 + (wv ? 1 : 0)) * sizeof(real);
+    prof_launch("aggregates", abytes, [&] {
+      launch(k_gram_mfma_f64, (unsigned)(nbx * gy), BLOCK, 0, Rp, L, (const double *const *)A, (const double *)B,
+             (const double *)wv, gpartd_.p, nout, rpb, gy);
+    }, 2.0 * Rp * L * 32 * 32);
+    const uint64_t ng = (uint64_t)L * 1024, cnt = ng + 65;
+    prof_launch("aggr_reduce", (double)nbx * cnt * 8, [&] {
+      launch(k_reduce_parts<real, double>, (unsigned)((cnt + 15) / 16), BLOCK, 0, nbx, nout, (uint64_t)0, cnt,
+             (const double *)gpartd_.p, ng, M, sums_.p);
     });
   }
 
@@ -2859,6 +2886,7 @@ template <typename real> class Problem final : public ProblemBase {
   uint64_t cgram_chunk_ = std::getenv("OCFFM_CGRAM_CHUNK") ? std::max(1, std::atoi(std::getenv("OCFFM_CGRAM_CHUNK"))) : 128;
   bool no_mfma_ = std::getenv("OCFFM_NO_MFMA") != nullptr;  // Grams on the VALU kernel instead
   DevBuf<float> gpart64_;  // k_gram_mfma64 partials
+  DevBuf<double> gpartd_;  // k_gram_mfma_f64 partials
   uint64_t gram64_blocks_ = std::getenv("OCFFM_GRAM64_BLOCKS") ? std::strtoull(std::getenv("OCFFM_GRAM64_BLOCKS"), nullptr, 10) : 1024;
   uint64_t gram_blocks_ = std::getenv("OCFFM_GRAM_BLOCKS") ? std::strtoull(std::getenv("OCFFM_GRAM_BLOCKS"), nullptr, 10) : 512;
   bool no_owned_ = false;

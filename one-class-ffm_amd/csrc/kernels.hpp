@@ -1374,6 +1374,69 @@ static __global__ __launch_bounds__(BLOCK) void k_col_gram32(uint64_t nchunks, c
   for (int r = 0; r < 16; r++) out[(8 * (r >> 2) + 4 * hf + (r & 3)) * 32 + e] = acc[r];
 }
 
+// The same in fp64 on the f64 matrix cores (v_mfma_f64_16x16x4f64, the
+// k_hot_gram_mfma_f64 operand layout: four rows per MFMA as K; tiles 00, 01,
+// 11 of the symmetric 32 x 32 Gram, 10 stored as 01^T); multi-chunk columns
+// summed by k_hot_slot_sum<double, 32>.
+static __global__ __launch_bounds__(BLOCK) void k_col_gram_f64(uint64_t nchunks, const Job *__restrict__ chunks,
+                                                              const uint32_t *__restrict__ crow,
+                                                              const double *__restrict__ cval,
+                                                              const int64_t *__restrict__ yptr,
+                                                              const double *__restrict__ Q1, uint64_t q1rows, double w,
+                                                              double n1, double *__restrict__ G,
+                                                              double *__restrict__ gpart) {
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  constexpr int NG = CGRAM32_ROWS / 4;
+  const int lane = threadIdx.x & 63;
+  const uint64_t wv = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+  if (wv >= nchunks) return;
+  const Job jb = chunks[wv];
+  const int n = (int)(jb.e - jb.b);  // <= CGRAM32_ROWS (host)
+  uint32_t il = 0;
+  double cl = 0.0;
+  if (lane < n) {
+    il = crow[jb.b + lane];
+    const double x = cval[jb.b + lane];
+    cl = ((1 - w) * (double)(yptr[il + 1] - yptr[il]) + w * n1) * x * x;
+  }
+  const BufView qb = buf_view(Q1, q1rows * 256);
+  const int c16 = lane & 15, rq = lane >> 4;
+  double q0[NG], q1[NG], cv[NG];
+#pragma unroll
+  for (int g = 0; g < NG; g++) {
+    const int r = 4 * g + rq;  // rows past n: weight 0, the loads read zero
+    const uint32_t i = (uint32_t)__shfl((int)il, r, 64);
+    cv[g] = __shfl(cl, r, 64);
+    const uint32_t off = r < n ? i * 256u + (uint32_t)c16 * 8u : 0xffffffffu;
+    q0[g] = bld1<double>(qb, off);
+    q1[g] = bld1<double>(qb, r < n ? off + 128u : 0xffffffffu);
+  }
+  d4 acc[2][3];
+#pragma unroll
+  for (int u = 0; u < 2; u++)
+#pragma unroll
+    for (int a = 0; a < 3; a++) acc[u][a] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int g = 0; g < NG; g++) {
+    d4(&c)[3] = acc[g & 1];
+    const double a0 = cv[g] * q0[g], a1 = cv[g] * q1[g];
+    c[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, q0[g], c[0], 0, 0, 0);
+    c[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, q1[g], c[1], 0, 0, 0);
+    c[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, q1[g], c[2], 0, 0, 0);
+  }
+#pragma unroll
+  for (int a = 0; a < 3; a++) acc[0][a] += acc[1][a];
+  double *out = jb.nparts <= 1 ? G + (size_t)jb.col * 1024 : gpart + (size_t)jb.slot * 1024;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int m = rq + 4 * r;
+    out[m * 32 + c16] = acc[0][0][r];
+    out[m * 32 + 16 + c16] = acc[0][1][r];
+    out[(16 + c16) * 32 + m] = acc[0][1][r];
+    out[(16 + m) * 32 + 16 + c16] = acc[0][2][r];
+  }
+}
+
 // G_c = sum of the partial slots of a multi-chunk column, in slot order
 // (sums: Job{col, nparts, first slot}).  One block per such column; thread t
 // owns elements 4t .. 4t+3; slots are read GB at a time (loads in flight).

@@ -2132,8 +2132,9 @@ template <typename real> class Problem final : public ProblemBase {
     F.gslots = slots;
   }
 
-  // fp32 at KP = 32: the Grams are built on MFMA (kernels.hpp k_col_gram32)
-  bool cgram32() const { return std::is_same<real, float>::value && kp_ == 32 && !no_mfma_; }
+  // KP = 32: the Grams are built on the matrix cores (kernels.hpp
+  // k_col_gram32, fp32; k_col_gram_f64, fp64)
+  bool cgram32() const { return kp_ == 32 && !no_mfma_; }
 
   // Side half whose CG steps run on per-column Grams (several ranks: each
   // builds its partial Grams, and every CG step all-reduces G_c p_c).
@@ -2317,6 +2318,18 @@ template <typename real> class Problem final : public ProblemBase {
             if (F.gsums.n)
               launch(k_gram_slot_sum, (unsigned)F.gsums.n, BLOCK, 0, (const Job *)F.gsums.p,
                      (const float *)F.gpart.p, (float *)F.gram.p);
+            return;
+          }
+        }
+        if constexpr (std::is_same<real, double>::value && KP == 32) {
+          if (cgram32()) {
+            launch(k_col_gram_f64, (unsigned)((F.gchunks.n + 3) / 4), BLOCK, 0, (uint64_t)F.gchunks.n,
+                   (const Job *)F.gchunks.p, (const uint32_t *)F.crow.p, (const double *)F.cval.p, hess_cnt(h),
+                   (const double *)h.Q1, (uint64_t)h.own->R, w_, hess_n1(h), (double *)F.gram.p,
+                   (double *)F.gpart.p);
+            if (F.gsums.n)
+              launch(k_hot_slot_sum<double, 32>, dim3((unsigned)F.gsums.n, (1024 + BLOCK - 1) / BLOCK), BLOCK, 0,
+                     (const Job *)F.gsums.p, (const double *)F.gpart.p, (double *)F.gram.p);
             return;
           }
         }

@@ -22,7 +22,7 @@ FAMILY = [  # (regex on the demangled kernel name, family as named by the librar
     (r"k_fin<\w+, \d+, 1\b", "hv_fin"), (r"k_gd_cross_seg", "gd_cross_row"), (r"k_gd_side_seg", "gd_side_row"),
     (r"k_update_cross_seg", "update_cross_row"), (r"k_update_side_row", "update_side_row"),
     (r"k_gather_pos", "refresh_base"), (r"k_gram_part", "aggregates"), (r"k_reduce_parts", "aggr_reduce"),
-    (r"k_gram_mfma32|k_gram_mfma64", "aggregates"), (r"k_rows_T", "rows_T"), (r"k_vec_sum", "bias_sum"), (r"k_pos_gram32|k_gram_rows", "aggregates"),
+    (r"k_gram_mfma32|k_gram_mfma64|k_gram_mfma_f64", "aggregates"), (r"k_rows_T", "rows_T"), (r"k_vec_sum", "bias_sum"), (r"k_pos_gram32|k_gram_rows", "aggregates"),
     (r"k_hs_cross_rc", "hs_cross_row"), (r"k_col_gram", "col_gram"), (r"k_hv_cgram", "hv_cgram"),
     (r"k_apply", "apply_step"), (r"k_rowdot_multi", "rowdot_multi"), (r"k_colsum_multi", "aggregates"),
     (r"k_cg_step", "cg_step"), (r"k_cg_r2", "cg_r2"), (r"k_hot_gram|k_gram_add_tau|k_hot_slot_sum", "ccg_build"),

@@ -170,6 +170,29 @@ def test_gradient_and_hv_fp32_k32(monkeypatch, env):
                 assert rel(H1, H0) <= 1e-4, ("hv", f1, f2, half, rel(H1, H0))
 
 
+@pytest.mark.parametrize("env", [{}, {"OCFFM_CGRAM": "2"}, {"OCFFM_CCG": "2"}, {"OCFFM_NO_MFMA": "1"}])
+def test_gradient_and_hv_fp64_k32(monkeypatch, env):
+    """fp64 at k = 32, where the k x k work runs on the f64 matrix cores
+    (v_mfma_f64_16x16x4f64: the cross-half aggregates k_gram_mfma_f64, the
+    side-half column Grams k_col_gram_f64 under OCFFM_CGRAM=2, the cross
+    column Grams k_hot_gram_mfma_f64 under OCFFM_CCG=2; OCFFM_NO_MFMA=1: the
+    VALU kernels): every half's gradient and Hessian-vector product within
+    1e-12 of the oracle's."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    ds = synth.kkbox(**KK_RC)
+    o, g = pair(ds, with_test=False)
+    rng = np.random.default_rng(3)
+    for f1 in range(o.f):
+        for f2 in range(f1, o.f):
+            for half in (0, 1):
+                G0, G1 = o.grad(f1, f2, half), g.grad(f1, f2, half)
+                assert rel(G1, G0) <= 1e-12, ("grad", f1, f2, half, rel(G1, G0))
+                v = rng.standard_normal(G0.size)
+                H0, H1 = o.hv(f1, f2, half, v), g.hv(f1, f2, half, v)
+                assert rel(H1, H0) <= 1e-12, ("hv", f1, f2, half, rel(H1, H0))
+
+
 def test_epochs_fp32_k32():
     """Two fp32 epochs at k = 32: objective of the fp32 state (evaluated in
     fp64) within 1e-3 of the oracle's; CG counts within 1 per half."""

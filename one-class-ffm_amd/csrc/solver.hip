@@ -88,6 +88,27 @@ struct KStat {
 };
 
 // ------------------------------------------------------------------- data
+// Item-owned CG steps of an item-id field's cross halves on several ranks
+// (OCFFM_ITEM_OWNED): rank q owns the items [j0, j1) (equal
+// chunks of `chunk` items) and holds ALL positives of its items (every
+// rank's users), as positive segments whose partner rows index the
+// all-gathered user table (Pg: rank r's users at rows [r cu, r cu + R_r)).
+// Its CG steps then gather, finalise its own columns and sum only the three
+// dot products, instead of all-reducing the D x k partials every step.
+template <typename real> struct ItemOwned {
+  uint64_t j0 = 0, j1 = 0, chunk = 0, nseg = 0;
+  DevBuf<Seg> segs;
+  DevBuf<uint32_t> segptr;
+  DevBuf<uint32_t> ycol;  // Pg row of each positive
+  DevBuf<uint32_t> segd;  // the segment's column (the item)
+  DevBuf<real> segx;
+  DevBuf<uint32_t> scrow;  // segment CSC over the owned columns
+  DevBuf<real> scval;
+  DevBuf<Job> sjobs;
+  uint64_t snjw = 0, snslot = 0;
+  DevBuf<double> shdots;
+};
+
 template <typename real> struct DevField {
   uint64_t D = 0, nnz = 0;
   DevBuf<int64_t> xptr;
@@ -133,6 +154,7 @@ template <typename real> struct DevField {
   uint64_t cslots = 0, cnpos = 0;
   DevBuf<uint32_t> segd;  // one: the node of each positive segment's row (no row indirection)
   DevBuf<real> segx;
+  std::unique_ptr<ItemOwned<real>> io;  // item-owned CG steps (item-id field, several ranks)
   // host copies kept until the segment CSC is built
   std::vector<int64_t> h_xptr;
   std::vector<uint32_t> h_xidx;
@@ -442,6 +464,7 @@ template <typename real> class Problem final : public ProblemBase {
     for (DevSide<real> *sd : {&U_, &V_})
       for (uint32_t fi = 0; fi < sd->F.size(); fi++)
         if (ccg_field_all(*sd->F[fi], *sd, sd == &U_, fi, U)) ccg_setup(*sd->F[fi], *sd);
+    if (io_mode_ != 0 && comm_.active() && (comm_.nranks > 1 || io_mode_ == 2) && C_ > 0) io_setup(U, V);
     // T pre-pass rows: the larger side that takes the pre-pass (tpre() also
     // bounds R for 32-bit buffer offsets, so test each side on its own)
     uint64_t tR = 0;
@@ -2478,11 +2501,205 @@ template <typename real> class Problem final : public ProblemBase {
   }
   // Exact residual norm (fp64 parity mode): not for owned fields
   // on several ranks, whose r / Hp rows are current on their owner only.
-  bool exact_r2(const HalfCtx &h) const { return exact_r2_ && !(comm_.active() && h.F->excl); }
+  bool exact_r2(const HalfCtx &h) const { return exact_r2_ && !(comm_.active() && (h.F->excl || h.F->io)); }
+
+  // ---- item-owned CG steps (OCFFM_ITEM_OWNED=1, the default: several
+  // ranks; 2: also a one-rank communicator, to run the collectives' code
+  // path; 0: off, every step all-reduces the D x k partials)
+  int io_mode_ = std::getenv("OCFFM_ITEM_OWNED") ? std::atoi(std::getenv("OCFFM_ITEM_OWNED")) : 1;
+  DevBuf<real> Pg_, qtqg_;
+  uint64_t io_cu_ = 0;  // user rows per rank slot of Pg
+  bool io_half(const HalfCtx &h) const { return h.cross && !h.user && h.F->io != nullptr; }
+
+  // In-place all-gather: rank r's `count` values at buf + r count.  RCCL:
+  // ncclAllGather; the host hook (tests, rehearsals) sums the buffer with
+  // every other slot zeroed (exact).
+  void allgather_dev(real *buf, uint64_t count) {
+    const uint64_t N = (uint64_t)comm_.nranks, r = (uint64_t)comm_.rank;
+    if (comm_.nccl) {
+      NCCLCHK(ncclAllGather(buf + r * count, buf, count, std::is_same<real, double>::value ? ncclDouble : ncclFloat,
+                            comm_.nccl, stream_));
+      return;
+    }
+    if (r) HIPCHK(hipMemsetAsync(buf, 0, r * count * sizeof(real), stream_));
+    if (r + 1 < N) HIPCHK(hipMemsetAsync(buf + (r + 1) * count, 0, (N - r - 1) * count * sizeof(real), stream_));
+    allreduce_dev(buf, N * count);
+  }
+
+  // Each item-id field of the item side (one node per item row, item j ->
+  // column j) gets its owned items' positives over all users, in the order
+  // one rank would hold them (users ascending per item), cut into the same
+  // segments; the segment CSC's jobs cover the owned columns only.
+  void io_setup(const HostData &U, const HostData &V) {
+    const uint64_t N = (uint64_t)comm_.nranks, q = (uint64_t)comm_.rank, m = U.m;
+    io_cu_ = (m + N - 1) / N;
+    const HostData &Vs = split_host(V);
+    bool any = false;
+    uint64_t need = 0;
+    for (uint32_t fi = 0; fi < V_.F.size(); fi++) {
+      DevField<real> &F = *V_.F[fi];
+      if (!F.one || F.D != n_ || F.excl) continue;
+      bool ident = Vs.xptr[fi].size() == n_ + 1;
+      for (uint64_t j = 0; j < n_ && ident; j++) ident = Vs.xptr[fi][j + 1] - Vs.xptr[fi][j] == 1 && Vs.xidx[fi][j] == j;
+      if (!ident) continue;
+      auto io = std::make_unique<ItemOwned<real>>();
+      io->chunk = (n_ + N - 1) / N;
+      io->j0 = std::min<uint64_t>(n_, q * io->chunk);
+      io->j1 = std::min<uint64_t>(n_, (q + 1) * io->chunk);
+      const uint64_t R = io->j1 - io->j0;
+      // item-major positives of the owned items (users ascending), as Pg rows
+      std::vector<int64_t> yp(R + 1, 0);
+      for (uint64_t p = 0; p < U.ycol.size(); p++) {
+        const uint64_t j = U.ycol[p];
+        if (j >= io->j0 && j < io->j1) yp[j - io->j0 + 1]++;
+      }
+      for (uint64_t r = 0; r < R; r++) yp[r + 1] += yp[r];
+      std::vector<uint32_t> yc((size_t)yp[R]);
+      std::vector<int64_t> cur(yp.begin(), yp.end() - 1);
+      for (uint64_t rk = 0; rk < N; rk++) {
+        const uint64_t g0 = m * rk / N, g1 = m * (rk + 1) / N;
+        for (uint64_t g = g0; g < g1; g++)
+          for (uint64_t p = U.yptr[g]; p < U.yptr[g + 1]; p++) {
+            const uint64_t j = U.ycol[p];
+            if (j >= io->j0 && j < io->j1) yc[(size_t)cur[j - io->j0]++] = (uint32_t)(rk * io_cu_ + (g - g0));
+          }
+      }
+      // segments (build_segments' cut) with their node, and the CSC jobs
+      std::vector<Seg> segs;
+      std::vector<uint32_t> segptr(R + 1, 0), sd;
+      std::vector<double> sx;
+      for (uint64_t r = 0; r < R; r++) {
+        segptr[r] = (uint32_t)segs.size();
+        const int64_t b = yp[r], e = yp[r + 1];
+        const uint32_t nrow = (uint32_t)std::max<int64_t>(1, (e - b + (int64_t)seg_len_ - 1) / (int64_t)seg_len_);
+        int64_t p = b;
+        do {
+          const int64_t t = std::min<int64_t>(e, p + (int64_t)seg_len_);
+          segs.push_back(Seg{(uint32_t)r, (nrow << 1) | (p == b ? 1u : 0u), p, t});
+          sd.push_back((uint32_t)(io->j0 + r));
+          sx.push_back(Vs.xval[fi][io->j0 + r]);
+          p = t;
+        } while (p < e);
+      }
+      segptr[R] = (uint32_t)segs.size();
+      io->nseg = segs.size();
+      std::vector<int64_t> xp(io->nseg + 1);
+      for (uint64_t t = 0; t <= io->nseg; t++) xp[t] = (int64_t)t;
+      std::vector<uint8_t> own(F.D, 0);
+      for (uint64_t j = io->j0; j < io->j1; j++) own[j] = 1;
+      std::vector<uint32_t> crow;
+      std::vector<double> cval;
+      std::vector<Job> jobs;
+      build_csc(io->nseg, F.D, xp.data(), sd.data(), sx.data(), nsg(), crow, cval, jobs, io->snslot, own.data());
+      io->segs.upload(segs);
+      io->segptr.upload(segptr);
+      io->ycol.upload(yc);
+      io->segd.upload(sd);
+      io->segx.upload(to_real(sx));
+      io->scrow.upload(crow);
+      io->scval.upload(to_real(cval));
+      io->sjobs.upload(jobs);
+      io->snjw = jobs.size() / nsg();
+      io->shdots.alloc(std::max<uint64_t>(io->snslot, 1) * 3);
+      need = std::max(need, io->nseg);
+      if (io->snslot * kp_ > wpart_.n) wpart_.alloc(io->snslot * kp_);
+      if (N * io->chunk * kp_ > S_.n) {  // the all-gathered CG vectors: N whole chunks
+        S_.alloc(N * io->chunk * kp_);
+        Vd_.alloc(N * io->chunk * kp_);
+      }
+      F.io = std::move(io);
+      any = true;
+    }
+    if (!any) return;
+    if (need * kp_ > h_.n) h_.alloc(need * kp_);
+    Pg_.alloc(N * io_cu_ * kp_);
+    qtqg_.alloc((uint64_t)kp_ * kp_);
+    const uint64_t st = std::max<uint64_t>(N * io_cu_, N * ((n_ + N - 1) / N)) * kp_;
+    if (comm_.host_fn && st > dmax_ * kp_) {
+      HIPCHK(hipHostFree(stage_));
+      HIPCHK(hipHostMalloc((void **)&stage_, st * sizeof(real), hipHostMallocDefault));
+    }
+  }
+
+  // Before the CG steps: every rank's rows of the partner (user) table and
+  // the global Q^T Q of this half.
+  void io_begin(HalfCtx &h) {
+    const uint64_t r = (uint64_t)comm_.rank, R = h.partner->R;
+    HIPCHK(hipMemsetAsync(Pg_.p + r * io_cu_ * kp_, 0, io_cu_ * kp_ * sizeof(real), stream_));
+    if (R) HIPCHK(hipMemcpyAsync(Pg_.p + r * io_cu_ * kp_, h.Q1, R * kp_ * sizeof(real), hipMemcpyDeviceToDevice, stream_));
+    allgather_dev(Pg_.p, io_cu_ * kp_);
+    HIPCHK(hipMemcpyAsync(qtqg_.p, qtq_, (size_t)kp_ * kp_ * sizeof(real), hipMemcpyDeviceToDevice, stream_));
+    allreduce_dev(qtqg_.p, (uint64_t)kp_ * kp_);
+  }
+  // After them: the owners' S and p columns on every rank (the update reads
+  // S + alpha p of every column).
+  void io_end(HalfCtx &h) {
+    const ItemOwned<real> &io = *h.F->io;
+    allgather_dev(S_.p, io.chunk * kp_);
+    allgather_dev(Vd_.p, io.chunk * kp_);
+  }
+  // One item-owned CG step: the owned items' rows over all users' positives,
+  // the owned columns' finalisation, the dot products summed over the ranks.
+  void hv_io(HalfCtx &h, int it) {
+    DevField<real> &F = *h.F;
+    const ItemOwned<real> &io = *F.io;
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      using Gm = Geo<real, KP>;
+      const double rs = sizeof(real);
+      const size_t qsz = (size_t)KP * KP * sizeof(real);
+      const bool lds = qsz <= 32 * 1024;
+      const bool ct = coltau(h);
+      Fin<real> fin = make_fin(h, it);
+      fin.dots = dots_.p;
+      const int *run = &st_.p->run[it];
+      if (io.nseg) {
+        prof_launch("hs_cross_io", (double)io.nseg * (24 + 8 + rs) + (double)io.nseg * KP * rs * 2, [&] {
+          auto go = [&](auto ml) {
+            constexpr bool ML = decltype(ml)::value;
+            launch(k_hs_cross_seg<real, KP, ML>, grid_for(io.nseg, 4 * Gm::NSG, hs_blocks_), BLOCK, lds ? qsz : 0,
+                   io.nseg, io.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, io.ycol.p, (const real *)Pg_.p,
+                   (uint64_t)comm_.nranks * io_cu_, ct ? (const real *)nullptr : (const real *)qtqg_.p, w_, h_.p,
+                   run, Rv_.p, Hv_.p, st_.p, it, io.segd.p, io.segx.p, (const uint32_t *)nullptr,
+                   (const real *)nullptr);
+          };
+          if (lds) go(std::true_type());
+          else go(std::false_type());
+        });
+      }
+      if (!io.snjw) {
+        HIPCHK(hipMemsetAsync(dots_.p, 0, 3 * sizeof(double), stream_));
+      } else {
+        fin.hdots = io.shdots.p;
+        fin.nhd = (uint32_t)io.snslot;
+        const unsigned grid = (unsigned)std::min<uint64_t>((io.snjw + 3) / 4, feat_blocks_);
+        prof_launch("feat_hv_io", (double)io.scrow.n * (4 + rs) * 2 + (double)io.snjw * Gm::NSG * sizeof(Job), [&] {
+          if constexpr ((size_t)KP * KP * sizeof(real) <= COLTAU_LDS) {
+            if (ct) {
+              fin.xsq = F.xsq.p;
+              launch(k_feat<real, KP, 1, JOB_ENT, true>, grid, BLOCK, (size_t)KP * KP * sizeof(real), io.snjw,
+                     io.sjobs.p, io.scrow.p, io.scval.p, h_.p, h_.bytes(), wpart_.p, wpart_.bytes(), fin,
+                     (const real *)qtqg_.p);
+              return;
+            }
+          }
+          launch(k_feat<real, KP, 1>, grid, BLOCK, 0, io.snjw, io.sjobs.p, io.scrow.p, io.scval.p, h_.p, h_.bytes(),
+                 wpart_.p, wpart_.bytes(), fin, (const real *)nullptr);
+        });
+      }
+      allreduce_dev_d(dots_.p, 3);
+      const Fin<real> f2 = fin;
+      prof_launch("cg_step", 0, [&] { launch(k_cg_step<real, 1>, 1, 64, 0, f2); });
+    });
+  }
 
   void hv_product(HalfCtx &h, int it) {
     DevSide<real> &own = *h.own;
     const int *run = &st_.p->run[it];
+    if (io_half(h)) {
+      hv_io(h, it);
+      return;
+    }
     if (cgram(h)) {
       with_kp(kp_, [&](auto K) {
         constexpr int KP = decltype(K)::value;
@@ -2604,10 +2821,11 @@ template <typename real> class Problem final : public ProblemBase {
     // The verdicts are global, so on several ranks every rank predicts and
     // queues the same sequence (the update itself has no collective).
     const size_t key = (size_t)h.b12 * 2 + (size_t)which;
-    const int pred = !spec_on_ || lookahead_ != 1 ? 0
-                     : spec_fixed_ > 0          ? spec_fixed_
-                     : key < pred_.size()       ? pred_[key]
-                                                : 0;
+    const bool io = io_half(h);  // (its update needs the all-gathered S and p: no speculative update)
+    const int pred = !spec_on_ || lookahead_ != 1 || io ? 0
+                     : spec_fixed_ > 0                ? spec_fixed_
+                     : key < pred_.size()             ? pred_[key]
+                                                      : 0;
     bool queued = false;
     const size_t pend0 = pending_.size();
     int it0 = 1;
@@ -2626,6 +2844,7 @@ template <typename real> class Problem final : public ProblemBase {
       gradient(h);
       col_grams(h);
       hot_grams(h);
+      if (io) io_begin(h);
     }
     for (int it = it0; it <= MAXCG && !done && !queued; it++) {
       prof_tag_ = it;
@@ -2642,6 +2861,7 @@ template <typename real> class Problem final : public ProblemBase {
       }
     }
     if (!done) examine(MAXCG);
+    if (io) io_end(h);
     if (!queued) finish_half(h, nullptr);
     if (key >= pred_.size()) pred_.resize(key + 1, 0);
     pred_[key] = nr;

@@ -192,12 +192,14 @@ def _gpu_worker(rank, port, out_dir, world, name="tiny"):
     g.set_profiling(True)
     for _ in range(2):
         g.one_epoch()
-    steps = g.kernel_stats().get("cg_step", {}).get("launches", 0)
+    ks = g.kernel_stats()
+    steps = ks.get("cg_step", {}).get("launches", 0)
+    io = ks.get("hs_cross_io", {}).get("launches", 0)
     met = g.validate()
     nb = g.n_blocks()
     W = [g.get("W", b) for b in range(nb)] + [g.get("H", b) for b in range(nb)]
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), cg=g.cg_log(), loss=met["loss"], ndcg=met["ndcg"],
-             prec=met["prec"], steps=steps, *W)
+             prec=met["prec"], steps=steps, io=io, *W)
     g.close()
     dist.destroy_process_group()
 
@@ -206,7 +208,10 @@ def _gpu_worker(rank, port, out_dir, world, name="tiny"):
 @pytest.mark.parametrize("name,env", [("tiny", {}), ("owned", {}), ("lowcard", {"OCFFM_CGRAM": "2"}),
                                       ("lowcard", {"OCFFM_CGRAM": "2", "OCFFM_FUSE": "0"}), ("outbrain", {}),
                                       ("outbrain", {"OCFFM_EXACT_R2": "1"}), ("owned", {"OCFFM_CCG": "2"}),
-                                      ("lowcard", {"OCFFM_CCG": "2", "OCFFM_HOT": "2"})])
+                                      ("lowcard", {"OCFFM_CCG": "2", "OCFFM_HOT": "2"}),
+                                      ("owned", {"OCFFM_ITEM_OWNED": "0"}),
+                                      ("owned", {"OCFFM_ITEM_OWNED": "0", "OCFFM_CCG": "2"}),
+                                      ("owned", {"OCFFM_EXACT_R2": "1"})])
 def test_two_ranks_match_one_rank_on_gpu(name, env, monkeypatch):
     import ocffm
     for k, v in env.items():  # inherited by the spawned ranks
@@ -223,8 +228,13 @@ def test_two_ranks_match_one_rank_on_gpu(name, env, monkeypatch):
             g.one_epoch()
         met = g.validate()
         nb = g.n_blocks()
-        # the owned-field path ran (listener-id halves) only where it applies
-        assert (int(r0["steps"]) > 0) == (name == "owned")
+        # the owned-field path ran on the listener-id halves, and the song-id
+        # item halves' CG steps ran item-owned (the default on several ranks)
+        # unless OCFFM_ITEM_OWNED=0
+        if name == "owned":
+            assert int(r0["steps"]) > 0
+            io_on = env.get("OCFFM_ITEM_OWNED", "1") != "0"
+            assert (int(r0["io"]) > 0) == io_on and (int(r1["io"]) > 0) == io_on
         np.testing.assert_array_equal(r0["cg"], g.cg_log())
         np.testing.assert_array_equal(r1["cg"], g.cg_log())
         for idx, (what, b) in enumerate([("W", b) for b in range(nb)] + [("H", b) for b in range(nb)]):
@@ -235,6 +245,34 @@ def test_two_ranks_match_one_rank_on_gpu(name, env, monkeypatch):
         assert abs(float(r0["loss"]) - met["loss"]) <= 1e-9 * met["loss"]
         np.testing.assert_allclose(r0["ndcg"], met["ndcg"], atol=1e-12)
         np.testing.assert_allclose(r0["prec"], met["prec"], atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_rccl_one_rank_item_owned():
+    """The item-owned CG steps through RCCL (ncclAllGather in place, the dot
+    products by ncclAllReduce) on a one-rank communicator (OCFFM_ITEM_OWNED=2
+    takes the path without a second rank): fp64 within 1e-9 of the plain run,
+    identical CG counts."""
+    import ocffm
+    ds = _dist_dataset("owned")
+    a = ocffm.problem_from_dataset(ds, precision=ocffm.FP64)
+    os.environ["OCFFM_ITEM_OWNED"] = "2"
+    try:
+        b = ocffm.problem_from_dataset(ds, precision=ocffm.FP64, rank=0, nranks=1, comm=ocffm.comm_id())
+    finally:
+        os.environ.pop("OCFFM_ITEM_OWNED", None)
+    b.set_profiling(True)
+    for g in (a, b):
+        ocffm.srand(1)
+        g.init()
+        for _ in range(2):
+            g.one_epoch()
+    assert b.kernel_stats().get("hs_cross_io", {}).get("launches", 0) > 0
+    np.testing.assert_array_equal(a.cg_log(), b.cg_log())
+    for bl in range(a.n_blocks()):
+        for what in "WH":
+            ref = a.get(what, bl)
+            assert np.abs(b.get(what, bl) - ref).max() <= 1e-9 * np.abs(ref).max(), (what, bl)
 
 
 @pytest.mark.gpu

@@ -2532,6 +2532,12 @@ template <typename real> class Problem final : public ProblemBase {
   // segments; the segment CSC's jobs cover the owned columns only.
   void io_setup(const HostData &U, const HostData &V) {
     const uint64_t N = (uint64_t)comm_.nranks, q = (uint64_t)comm_.rank, m = U.m;
+    // Worth it where the user table's all-gather (m k) plus S and p (2 n k)
+    // moves less than the ring all-reduces of ~8 CG steps (8 x 2 n k): m <=
+    // 14 n (kkbox at N = 8: 246 k users, 100 k items; not config 5: 100 M
+    // users against 250 k items), and the gathered table within 8 GB.
+    if (io_mode_ == 1 && (double)m > 14.0 * (double)n_) return;
+    if ((double)N * ((m + N - 1) / N) * kp_ * sizeof(real) > 8e9) return;
     io_cu_ = (m + N - 1) / N;
     const HostData &Vs = split_host(V);
     bool any = false;

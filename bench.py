@@ -280,6 +280,10 @@ def main():
                        "rccl_ranks": world if comm is not None else 0,
                        "launcher": os.environ.get("OCFFM_BENCH_LAUNCHER", "torchrun" if world > 1 else "none"),
                        "allreduce": "gloo-host (rehearsal)" if rehearsal else ("rccl" if comm is not None else "none"),
+                       # song-id item halves' CG steps item-owned (the library's
+                       # gate: several ranks, users <= 14 x items)
+                       "item_owned_cg": bool(world > 1 and os.environ.get("OCFFM_ITEM_OWNED", "1") != "0"
+                                             and rows_total <= 14 * int(ds.item.m)),
                        "cg_iters_per_epoch": r["cg_per_epoch"]},
             "roofline": r["roof"],
             "cpu_baseline": cpu,

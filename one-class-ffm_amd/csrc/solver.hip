@@ -2535,9 +2535,10 @@ template <typename real> class Problem final : public ProblemBase {
     // Worth it where the user table's all-gather (m k) plus S and p (2 n k)
     // moves less than the ring all-reduces of ~8 CG steps (8 x 2 n k): m <=
     // 14 n (kkbox at N = 8: 246 k users, 100 k items; not config 5: 100 M
-    // users against 250 k items), and the gathered table within 8 GB.
+    // users against 250 k items), and the gathered table within the 32-bit
+    // offsets of the partner-row gathers (BufView).
     if (io_mode_ == 1 && (double)m > 14.0 * (double)n_) return;
-    if ((double)N * ((m + N - 1) / N) * kp_ * sizeof(real) > 8e9) return;
+    if ((double)N * ((m + N - 1) / N) * kp_ * sizeof(real) >= (double)((1ull << 32) - 64)) return;
     io_cu_ = (m + N - 1) / N;
     const HostData &Vs = split_host(V);
     bool any = false;
@@ -2618,6 +2619,8 @@ template <typename real> class Problem final : public ProblemBase {
     }
     if (!any) return;
     if (need * kp_ > h_.n) h_.alloc(need * kp_);
+    if (h_.bytes() >= (1ull << 32) - 64)  // kernels.hpp: BufView gathers use 32-bit offsets
+      throw Error(OCFFM_E_DATA, "too many item-owned segments per GPU for one partial buffer; set OCFFM_ITEM_OWNED=0");
     Pg_.alloc(N * io_cu_ * kp_);
     qtqg_.alloc((uint64_t)kp_ * kp_);
     const uint64_t st = std::max<uint64_t>(N * io_cu_, N * ((n_ + N - 1) / N)) * kp_;

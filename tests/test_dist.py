@@ -167,6 +167,10 @@ def _dist_dataset(name):
         # rank); their cross halves take the column-tau term before the all-reduce
         return synth.general(seed=23, m=300, n=200, fu=2, fv=2, k=8, d_user=[300, 6], d_item=[200, 5],
                              nnz_user=1, mean_pos=5.0, test_rows=30, name="lowcard")
+    if name == "one_item":
+        # a single item: with two ranks the second owns no item at all
+        # (item-owned CG steps forced by OCFFM_ITEM_OWNED=2)
+        return synth.kkbox(seed=6, m=200, n=1, mean=1.0, name="one_item")
     if name == "outbrain":
         # BASELINE configs[3]'s data-parallel workload at test size (SURVEY
         # §8d): fu = 2, fv = 2, k = 64, ~1 positive per row
@@ -211,7 +215,7 @@ def _gpu_worker(rank, port, out_dir, world, name="tiny"):
                                       ("lowcard", {"OCFFM_CCG": "2", "OCFFM_HOT": "2"}),
                                       ("owned", {"OCFFM_ITEM_OWNED": "0"}),
                                       ("owned", {"OCFFM_ITEM_OWNED": "0", "OCFFM_CCG": "2"}),
-                                      ("owned", {"OCFFM_EXACT_R2": "1"})])
+                                      ("owned", {"OCFFM_EXACT_R2": "1"}), ("one_item", {"OCFFM_ITEM_OWNED": "2"})])
 def test_two_ranks_match_one_rank_on_gpu(name, env, monkeypatch):
     import ocffm
     for k, v in env.items():  # inherited by the spawned ranks
@@ -235,6 +239,8 @@ def test_two_ranks_match_one_rank_on_gpu(name, env, monkeypatch):
             assert int(r0["steps"]) > 0
             io_on = env.get("OCFFM_ITEM_OWNED", "1") != "0"
             assert (int(r0["io"]) > 0) == io_on and (int(r1["io"]) > 0) == io_on
+        if name == "one_item":  # rank 1 owns no item: it only joins the collectives
+            assert int(r0["io"]) > 0 and int(r1["io"]) == 0
         np.testing.assert_array_equal(r0["cg"], g.cg_log())
         np.testing.assert_array_equal(r1["cg"], g.cg_log())
         for idx, (what, b) in enumerate([("W", b) for b in range(nb)] + [("H", b) for b in range(nb)]):

@@ -37,6 +37,7 @@ import argparse
 import glob
 import json
 import os
+import re
 import resource
 import socket
 import subprocess
@@ -180,10 +181,15 @@ def run_newton(ds, prec, steps, warmup, k=32, self_side=True, world=1, rank=0, l
                                    for kk, v in sorted(fams.items(), key=lambda kv: -kv[1]["total_ms"])[:6]}})
     # HBM bytes per launch of the same kernel family from the committed
     # rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, MI355X guide §HBM).
-    pat = f"r*_{pmc_tag}pmc_traffic.json"
-    pmcs = sorted(p for p in glob.glob(os.path.join(REPO, "profiles", pat)) if pmc_tag or "_sgd_" not in p
-                  and "_cfg5_" not in p and "_fp64_" not in p)
-    if pmcs:
+    # Those passes are one-GPU runs: on several ranks nobody measured this
+    # run's counters, so the line carries null (and says why).
+    # (rNN[a-z]_<tag>pmc_traffic.json: the headline's tag is empty)
+    name_re = re.compile(r"^r\d+[a-z]?_" + re.escape(pmc_tag) + r"pmc_traffic\.json$")
+    pmcs = sorted(p for p in glob.glob(os.path.join(REPO, "profiles", "r*pmc_traffic.json"))
+                  if name_re.match(os.path.basename(p)))
+    if world > 1:
+        roof["traffic_source"] = "none: the committed PMC passes are N=1 runs"
+    elif pmcs:
         pmc = pmcs[-1]
         roof["traffic_source"] = os.path.relpath(pmc, REPO)
         try:
@@ -191,8 +197,11 @@ def run_newton(ds, prec, steps, warmup, k=32, self_side=True, world=1, rank=0, l
             roof["traffic"] = None if t is None else round(t["bytes_per_launch"])
         except Exception:
             pass
+    # what ran, observed (not re-derived from the library's gate): the
+    # item-owned CG steps' row pass appears in the kernel-timing pass
+    io_launches = int(ks.get("hs_cross_io", {}).get("launches", 0))
     return dict(dt=dt, roof=roof, cg_per_epoch=round(cg.sum() / max(1, steps), 1),
-                setup_s={"create": round(t_create, 3), "init": round(t_init, 3)})
+                setup_s={"create": round(t_create, 3), "init": round(t_init, 3)}, io_launches=io_launches)
 
 
 def main():
@@ -261,6 +270,8 @@ def main():
     if world == 1 and args.modes == "auto":
         if prec == ocffm.FP32:
             modes["fp64"] = timed_mode(fp64_mode, ds, args)
+        modes["kdd12"] = timed_mode(shape_mode, args, "kdd12")
+        modes["outbrain"] = timed_mode(shape_mode, args, "outbrain")
         modes["cfg5"] = timed_mode(cfg5_mode, args)
         if args.sgd == "auto":
             modes["sgd"] = timed_mode(sgd_mode, ds, args)
@@ -280,10 +291,10 @@ def main():
                        "rccl_ranks": world if comm is not None else 0,
                        "launcher": os.environ.get("OCFFM_BENCH_LAUNCHER", "torchrun" if world > 1 else "none"),
                        "allreduce": "gloo-host (rehearsal)" if rehearsal else ("rccl" if comm is not None else "none"),
-                       # song-id item halves' CG steps item-owned (the library's
-                       # gate: several ranks, users <= 14 x items)
-                       "item_owned_cg": bool(world > 1 and os.environ.get("OCFFM_ITEM_OWNED", "1") != "0"
-                                             and rows_total <= 14 * int(ds.item.m)),
+                       # song-id item halves' CG steps item-owned: observed,
+                       # launches of their row pass in the kernel-timing pass
+                       "item_owned_cg": r["io_launches"] > 0,
+                       "item_owned_cg_launches": r["io_launches"],
                        "cg_iters_per_epoch": r["cg_per_epoch"]},
             "roofline": r["roof"],
             "cpu_baseline": cpu,
@@ -319,6 +330,37 @@ def fp64_mode(ds, args):
         return {"metric": "train instances/sec, kkbox-shape k=32, fp64 (parity mode)",
                 "value": round(ROWS_PER_GPU * args.steps / r["dt"], 1), "unit": "instances/s", "dtype": "f64",
                 "ms_per_step": round(r["dt"] / args.steps * 1e3, 3), "cg_iters_per_epoch": r["cg_per_epoch"],
+                "roofline": r["roof"]}
+    except Exception as e:  # never blocks the headline number
+        return {"value": None, "error": str(e)}
+
+
+SHAPES = {  # BASELINE configs at their SURVEY §8d per-GPU sizes (synth.kdd12 / synth.outbrain)
+    "kdd12": dict(k=16, workload="BASELINE configs[1] shape (SURVEY §8d): kdd12, 500 k users x 50 k ads, "
+                              "user fields UserID + {QueryID, Depth}, ad fields Title, Description, Keyword, "
+                              "{AdID, DisplayURL, Advertiser}, k=16, squared loss (the reference has no log-loss)"),
+    "outbrain": dict(k=64, workload="BASELINE configs[3] shape (SURVEY §8d): one GPU's 250 k-row shard of the "
+                                    "2 M-row 8-GPU run, 10 k ads, 2 + 2 multi-node fields, ~1 positive per row, k=64"),
+}
+
+
+def shape_mode(args, name):
+    """One of BASELINE's other configs at its per-GPU size, fp32, with its
+    own roofline (the same measurement as the headline line)."""
+    try:
+        t0 = time.perf_counter()
+        ds = getattr(synth, name)()
+        gen = time.perf_counter() - t0
+        sh = SHAPES[name]
+        r = run_newton(ds, ocffm.FP32, args.steps, args.warmup, k=sh["k"], pmc_tag=name + "_")
+        return {"metric": f"train instances/sec, {name}-shape k={sh['k']}",
+                "value": round(ds.train.m * args.steps / r["dt"], 1), "unit": "instances/s", "dtype": "f32",
+                "ms_per_step": round(r["dt"] / args.steps * 1e3, 3),
+                "config": {"workload": sh["workload"], "rows_per_gpu": ds.train.m, "items": int(ds.item.m),
+                           "positives": ds.n_positives, "user_fields": int(ds.train.fid.max()) + 1,
+                           "item_fields": int(ds.item.fid.max()) + 1, "k": sh["k"],
+                           "cg_iters_per_epoch": r["cg_per_epoch"], "datagen_s": round(gen, 2),
+                           "setup_s": r["setup_s"]},
                 "roofline": r["roof"]}
     except Exception as e:  # never blocks the headline number
         return {"value": None, "error": str(e)}
@@ -396,7 +438,21 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline(ds, epochs, single_epochs=1, snap=None, gpu_cg=None):
+def _physical_cores():
+    """(physical id, core id) pairs of /proc/cpuinfo: cores, not SMT threads."""
+    try:
+        cores, phys = set(), None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                phys = line.split(":", 1)[1].strip()
+            elif line.startswith("core id"):
+                cores.add((phys, line.split(":", 1)[1].strip()))
+        return len(cores) or None
+    except OSError:
+        return None
+
+
+def cpu_baseline(ds, epochs, single_epochs=1, snap=None, gpu_cg=None, all_epochs=1):
     """The CPU oracle on a bounded sample: `epochs` epochs of the same
     kkbox-shaped problem, fp64, on every host core this process may use.
     With `snap` (the GPU's tables after its warm-up) the oracle starts from
@@ -427,6 +483,13 @@ def cpu_baseline(ds, epochs, single_epochs=1, snap=None, gpu_cg=None):
                         "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}}
         if gpu_cg:  # the same rate per CG step (the work an epoch does scales with its CG steps)
             out["value_at_gpu_cg_count"] = round(out["value"] * cg / gpu_cg, 1)
+        # SURVEY 8(d)'s -c <all cores>: every CPU this process may run on
+        # (the box exposes the whole host; its fair share is OMP_NUM_THREADS)
+        out["host"]["physical_cores"] = _physical_cores()
+        if avail > threads and all_epochs > 0:
+            sa = o.time_epochs(all_epochs, avail)
+            out["all_threads"] = {"value": round(ds.train.m * all_epochs / sa, 1), "cores": avail,
+                                  "sample": f"{all_epochs} epoch(s) after the sample above, {sa:.2f} s"}
         if single_epochs > 0:  # also the one-thread rate (the reference's -c 1)
             s1 = o.time_epochs(single_epochs, 1)
             out["single_thread"] = {"value": round(ds.train.m * single_epochs / s1, 1), "cores": 1,

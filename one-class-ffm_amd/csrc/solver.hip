@@ -474,7 +474,6 @@ template <typename real> class Problem final : public ProblemBase {
   }
 
   ~Problem() override {
-    clear_graphs();
     if (run_host_) (void)hipHostFree(run_host_);
     if (stage_) (void)hipHostFree(stage_);
     if (dstage_) (void)hipHostFree(dstage_);
@@ -570,7 +569,6 @@ template <typename real> class Problem final : public ProblemBase {
   std::chrono::steady_clock::time_point tmark_t_;
 
   void init() override {
-    clear_graphs();
     ysum_dirty();
     // a previous epoch that threw inside the cross loop may have left the
     // block-excluded form on: the base is rebuilt below from scratch
@@ -702,7 +700,6 @@ template <typename real> class Problem final : public ProblemBase {
         }
       }
     if (std::fgetc(fp) != EOF) throw Error(OCFFM_E_DATA, "binary model: trailing bytes after the last block");
-    clear_graphs();
     ysum_dirty();
     excl_ = ExclBase{};
     lazy_ok_ = false;
@@ -1494,11 +1491,6 @@ template <typename real> class Problem final : public ProblemBase {
   template <typename... KArgs, typename... A>
   void launch(void (*k)(KArgs...), dim3 grid, dim3 block, size_t smem, A... a) {
     static_assert(sizeof...(KArgs) == sizeof...(A), "kernel argument count");
-    if (capturing_) {  // inside a hipGraph capture (graph mode, no profiling)
-      k<<<grid, block, smem, stream_>>>(static_cast<KArgs>(a)...);
-      HIPCHK(hipGetLastError());
-      return;
-    }
     hipEvent_t e0 = arm_first_ ? arm_a_ : nullptr;
     arm_first_ = false;
     hipExtLaunchKernelGGL(k, grid, block, (uint32_t)smem, stream_, e0, arm_b_, 0u, static_cast<KArgs>(a)...);
@@ -2194,33 +2186,72 @@ template <typename real> class Problem final : public ProblemBase {
   // side's rows (all items) are the same on every rank; its positives and
   // the user side's rows are the shard's.
   bool ccg_field_all(const DevField<real> &F, const DevSide<real> &own, bool user, uint32_t fi,
-                     const HostData &U) const {
+                     const HostData &U) {
     if (!ccg_field(F, own)) return false;
     if (comm_.nranks == 1) return true;
-    const Rows &raw = U.raw;
     const uint64_t N = (uint64_t)comm_.nranks;
+    if (user && shard_facts_.empty()) shard_facts_ = shard_field_facts(U, N);
     for (uint64_t q = 0; q < N; q++) {
       const uint64_t u0 = U.m * q / N, u1 = U.m * (q + 1) / N;
       const uint64_t npos = U.yptr[u1] - U.yptr[u0];
       bool one = F.one, idl = F.idlike;
       if (user) {
-        one = u1 > u0;
-        std::vector<uint8_t> seen(F.D == u1 - u0 ? F.D : 0, 0);
-        idl = !seen.empty();
-        for (uint64_t i = u0; i < u1 && one; i++) {
-          uint32_t c = 0;
-          uint64_t x = 0;
-          for (uint64_t p = raw.xptr[i]; p < raw.xptr[i + 1]; p++)
-            if (raw.fid[p] == fi) c++, x = raw.idx[p];
-          one = c == 1;
-          if (idl && one) idl = !seen[x], seen[x] = 1;
-        }
-        idl = idl && one;
+        const uint8_t fact = shard_facts_[q * U_.F.size() + fi];
+        one = fact & 1;
+        idl = (fact & 2) != 0;
       }
       if (!ccg_pred(F.D, one, idl, npos, user ? u1 - u0 : own.R)) return false;
     }
     return true;
   }
+  // Per (user shard q, user field f), in ONE pass over the raw nodes: bit 0
+  // = every row of the shard has exactly one node of f (and the shard has
+  // rows), bit 1 = also no feature of f twice in the shard with D_f = its
+  // rows (an id-like field on that shard).  O(nnz) for all fields together.
+  std::vector<uint8_t> shard_field_facts(const HostData &U, uint64_t N) const {
+    const Rows &raw = U.raw;
+    const uint32_t nf = (uint32_t)U_.F.size();
+    std::vector<uint8_t> facts(N * nf, 0);
+    std::vector<uint32_t> cnt(nf, 0);
+    std::vector<uint64_t> ones(nf, 0);
+    std::vector<std::vector<uint8_t>> seen(nf);
+    for (uint64_t q = 0; q < N; q++) {
+      const uint64_t u0 = U.m * q / N, u1 = U.m * (q + 1) / N;
+      std::vector<uint8_t> idl(nf, 0);
+      for (uint32_t f = 0; f < nf; f++) {
+        const uint64_t D = U_.F[f]->D;
+        idl[f] = D == u1 - u0 && u1 > u0;
+        seen[f].assign(idl[f] ? D : 0, 0);
+        ones[f] = 0;
+      }
+      // per row: count each field's nodes, then visit the nodes again (each
+      // field once: its count is reset on the first visit)
+      for (uint64_t i = u0; i < u1; i++) {
+        const uint64_t b = raw.xptr[i], e = raw.xptr[i + 1];
+        for (uint64_t p = b; p < e; p++)
+          if (raw.fid[p] < nf) cnt[raw.fid[p]]++;
+        for (uint64_t p = b; p < e; p++) {
+          const uint32_t f = raw.fid[p];
+          if (f >= nf || cnt[f] == 0) continue;
+          if (cnt[f] == 1) {
+            ones[f]++;
+            const uint64_t x = raw.idx[p];
+            if (idl[f]) {
+              if (x < seen[f].size() && !seen[f][x]) seen[f][x] = 1;
+              else idl[f] = 0;
+            }
+          }
+          cnt[f] = 0;
+        }
+      }
+      for (uint32_t f = 0; f < nf; f++) {
+        const bool one = u1 > u0 && ones[f] == u1 - u0;
+        facts[q * nf + f] = (uint8_t)((one ? 1 : 0) | ((one && idl[f]) ? 2 : 0));
+      }
+    }
+    return facts;
+  }
+  std::vector<uint8_t> shard_facts_;  // shard_field_facts, computed on first use
   bool ccg_eligible(const HalfCtx &h) const { return h.cross && h.F->ccg_ready; }
   void ccg_setup(DevField<real> &F, DevSide<real> &own) {
     if (F.ccg_ready) return;
@@ -2501,7 +2532,7 @@ template <typename real> class Problem final : public ProblemBase {
   }
   // Exact residual norm (fp64 parity mode): not for owned fields
   // on several ranks, whose r / Hp rows are current on their owner only.
-  bool exact_r2(const HalfCtx &h) const { return exact_r2_ && !(comm_.active() && (h.F->excl || h.F->io)); }
+  bool exact_r2(const HalfCtx &h) const { return exact_r2_ && !(comm_.active() && (h.F->excl || io_half(h))); }
 
   // ---- item-owned CG steps (OCFFM_ITEM_OWNED=1, the default: several
   // ranks; 2: also a one-rank communicator, to run the collectives' code
@@ -2837,31 +2868,20 @@ template <typename real> class Problem final : public ProblemBase {
                                                       : 0;
     bool queued = false;
     const size_t pend0 = pending_.size();
-    int it0 = 1;
     const int last = key < pred_.size() ? pred_[key] : 0;
     ccg_now_ = ccg_eligible(h) && (ccg_mode_ == 2 || last >= 3);
     hot_now_ = last >= hot_steps_;
-    // Graph mode (OCFFM_GRAPH=1, one GPU, no profiling): the half's
-    // gradient, its first `pred` CG steps and the guarded update as one
-    // captured hipGraph, replayed in later epochs (measured).
-    if (graph_on_ && !profiling && !comm_.active() && pred >= 1 && pred < MAXCG) {
-      graph_half(h, which, pred);
-      examine(pred + 1);
-      queued = done;  // stopped by iteration pred: the graph's guarded update ran
-      it0 = pred + 1;
-    } else {
-      gradient(h);
-      col_grams(h);
-      hot_grams(h);
-      if (io) io_begin(h);
-    }
-    for (int it = it0; it <= MAXCG && !done && !queued; it++) {
+    gradient(h);
+    col_grams(h);
+    hot_grams(h);
+    if (io) io_begin(h);
+    for (int it = 1; it <= MAXCG && !done && !queued; it++) {
       prof_tag_ = it;
       hv_pass(h, it);
       prof_tag_ = 0;
       const int t = it - lookahead_;
       if (t >= 1) examine(t + 1);  // upd(t) decided run[t+1]
-      if (!done && it == pred && it < MAXCG && it0 == 1) {
+      if (!done && it == pred && it < MAXCG) {
         prof_tag_ = -1;
         finish_half(h, &st_.p->run[it + 1]);
         prof_tag_ = 0;
@@ -2891,75 +2911,6 @@ template <typename real> class Problem final : public ProblemBase {
       std::snprintf(name, sizeof(name), "half(%u,%u)%c", f1, f2, which ? 'H' : 'W');
       pending_.push_back({name, 0.0, hb, he, 0, 0.0});
     }
-  }
-
-  // ---- graph mode: the host state the half's enqueue logic reads and
-  // writes (block-excluded base, segment-sum validity, the CG QTQ pointer,
-  // owned-table staleness); a graph captured from one state is replayed
-  // only from that state, and leaves the host state its capture left.
-  struct HostState {
-    bool excl_on, ys0, ys1, owned_stale, lazy_ok;
-    uint32_t excl_b12;
-    const real *qtq;
-    bool operator<(const HostState &o) const {
-      return std::tie(excl_on, ys0, ys1, owned_stale, lazy_ok, excl_b12, qtq) <
-             std::tie(o.excl_on, o.ys0, o.ys1, o.owned_stale, o.lazy_ok, o.excl_b12, o.qtq);
-    }
-  };
-  HostState host_state() const {
-    return HostState{excl_.on, ysum_ok_[0], ysum_ok_[1], owned_stale_, lazy_ok_, excl_.b12, qtq_};
-  }
-  void set_host_state(const HostState &s) {
-    excl_.on = s.excl_on;
-    excl_.b12 = s.excl_b12;
-    ysum_ok_[0] = s.ys0;
-    ysum_ok_[1] = s.ys1;
-    owned_stale_ = s.owned_stale;
-    qtq_ = s.qtq;
-  }
-  struct GraphEntry {
-    hipGraphExec_t exec = nullptr;
-    HostState post;
-  };
-  std::map<std::tuple<uint32_t, int, int, HostState>, GraphEntry> graphs_;
-  bool graph_on_ = std::getenv("OCFFM_GRAPH") && std::atoi(std::getenv("OCFFM_GRAPH")) != 0;
-  bool capturing_ = false;
-
-  void clear_graphs() {
-    for (auto &g : graphs_) (void)hipGraphExecDestroy(g.second.exec);
-    graphs_.clear();
-  }
-
-  void graph_half(HalfCtx &h, int which, int pred) {
-    const auto key = std::make_tuple(h.b12, which, pred, host_state());
-    auto itg = graphs_.find(key);
-    if (itg == graphs_.end()) {
-      HIPCHK(hipStreamBeginCapture(stream_, hipStreamCaptureModeRelaxed));
-      capturing_ = true;
-      try {
-        gradient(h);
-        col_grams(h);
-        hot_grams(h);
-        for (int it = 1; it <= pred; it++) hv_pass(h, it);
-        finish_half(h, &st_.p->run[pred + 1]);
-      } catch (...) {
-        capturing_ = false;
-        hipGraph_t g = nullptr;
-        (void)hipStreamEndCapture(stream_, &g);
-        if (g) (void)hipGraphDestroy(g);
-        throw;
-      }
-      capturing_ = false;
-      hipGraph_t g = nullptr;
-      HIPCHK(hipStreamEndCapture(stream_, &g));
-      GraphEntry e;
-      HIPCHK(hipGraphInstantiate(&e.exec, g, nullptr, nullptr, 0));
-      HIPCHK(hipGraphDestroy(g));
-      e.post = host_state();
-      itg = graphs_.emplace(key, e).first;
-    }
-    set_host_state(itg->second.post);
-    HIPCHK(hipGraphLaunch(itg->second.exec, stream_));
   }
 
   // The end of a half: apply S (W += S, the last pending S += alpha p) and

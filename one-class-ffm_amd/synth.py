@@ -250,6 +250,85 @@ def cfg5(m: int = 2_000_000, n: int = 250_000, fu: int = 39, d_user: int = 250_0
                    params=dict(k=k, t=20, l=4.0, w=0.0078125, r=-1.0))
 
 
+def _skewed(rng, size, d, salt=0):
+    """Feature ids in [0, d): half uniform, half a Lomax(1.2) head (permuted
+    per salt so that the heads of different columns are different ids)."""
+    uni = rng.integers(0, d, size=size)
+    par = np.minimum(np.floor(rng.pareto(1.2, size=size)), d - 1).astype(np.int64)
+    par = (par * 7919 + salt * 104729) % d
+    return np.where(rng.random(size) < 0.5, uni, par).astype(np.uint64)
+
+
+def _multi_field(rng, count, parts, salt):
+    """One field made of several id columns (the reference's data-prep puts
+    e.g. QueryID and Depth into one field, kdd12.tools/user_ffm.py:5-7): each
+    column c has its own block of the field's index space [off_c, off_c + d_c)."""
+    cols, off = [], 0
+    for c, d in enumerate(parts):
+        cols.append(_skewed(rng, count, d, salt * 16 + c) + np.uint64(off))
+        off += d
+    return np.stack(cols, axis=1), off
+
+
+def kdd12(m: int = 500_000, n: int = 50_000, mean_pos: float = 3.0, seed: int = 12, test_rows: int = 0,
+          name: str = "kdd12") -> Dataset:
+    """BASELINE configs[1] at its SURVEY §8d size, vectorised: m = 500 k users,
+    n = 50 k ads, k = 16, ~3 positives per row.  Field structure of the
+    reference's data prep: user fields UserID (an id, one node) and
+    {QueryID, Depth} (two nodes; kdd12.tools/user_ffm.py:5-7); ad fields
+    TitleID, DescriptionID, KeywordID (one node each) and {AdID, DisplayURL,
+    AdvertiserID} (three nodes; kdd12.tools/ad_ffm.py:5-9).  The reference's
+    loss is squared (it has no log-loss), so this is its ffm-ffm
+    mode on that shape."""
+    rng = np.random.default_rng(seed)
+    ptr, col = _positives(rng, m, n, mean_pos)
+    uid = np.arange(m, dtype=np.uint64)[:, None]
+    q, _ = _multi_field(rng, m, [max(2, m // 5), 3], 1)
+    train = _fast_rows(m, [(0, uid, np.ones((m, 1))), (1, q, np.ones((m, 2)))], ptr, col)
+    t0 = _skewed(rng, n, max(2, n // 2), 2)[:, None]
+    t1 = _skewed(rng, n, max(2, n // 2), 3)[:, None]
+    t2 = _skewed(rng, n, max(2, n // 5), 4)[:, None]
+    ad = np.arange(n, dtype=np.uint64)[:, None]
+    rest, _ = _multi_field(rng, n, [max(2, n // 10), max(2, n // 50)], 5)
+    t3 = np.concatenate([ad, rest + np.uint64(n)], axis=1)
+    item = _fast_rows(n, [(0, t0, np.ones((n, 1))), (1, t1, np.ones((n, 1))), (2, t2, np.ones((n, 1))),
+                          (3, t3, np.ones((n, 3)))])
+    test = None
+    if test_rows:
+        tptr, tcol = _positives(rng, test_rows, n, mean_pos)
+        tq, _ = _multi_field(rng, test_rows, [max(2, m // 5), 3], 1)
+        test = _fast_rows(test_rows, [(0, uid[:test_rows], np.ones((test_rows, 1))),
+                                      (1, tq, np.ones((test_rows, 2)))], tptr, tcol)
+    return Dataset(name, train, item, test, k=16, params=dict(k=16, t=20, l=4.0, w=0.00048828125, r=-1.0))
+
+
+def outbrain(m: int = 250_000, n: int = 10_000, mean_pos: float = 1.0, seed: int = 13, test_rows: int = 0,
+             name: str = "outbrain") -> Dataset:
+    """BASELINE configs[3] per GPU (2 M display rows over 8 GPUs
+    = 250 k rows per GPU), vectorised: n = 10 k ads, k = 64, ~1 positive
+    per row (one click per display, outbrain.tools/add_label.py).  Context
+    fields {platform, geo_location} and {source_id, publisher_id,
+    document_id} (outbrain.tools/context_ffm.py:6-7); ad fields {source_id,
+    publisher_id, document_id} and {campaign_id, advertiser_id}
+    (outbrain.tools/item_ffm.py:6-7)."""
+    rng = np.random.default_rng(seed)
+    ptr, col = _positives(rng, m, n, mean_pos)
+    c0, _ = _multi_field(rng, m, [3, 2000], 1)
+    c1, _ = _multi_field(rng, m, [5000, 1000, 100_000], 2)
+    train = _fast_rows(m, [(0, c0, np.ones((m, 2))), (1, c1, np.ones((m, 3)))], ptr, col)
+    i0, _ = _multi_field(rng, n, [5000, 1000, 100_000], 3)
+    i1, _ = _multi_field(rng, n, [max(2, n // 3), max(2, n // 10)], 4)
+    item = _fast_rows(n, [(0, i0, np.ones((n, 3))), (1, i1, np.ones((n, 2)))])
+    test = None
+    if test_rows:
+        tptr, tcol = _positives(rng, test_rows, n, mean_pos)
+        t0, _ = _multi_field(rng, test_rows, [3, 2000], 1)
+        t1, _ = _multi_field(rng, test_rows, [5000, 1000, 100_000], 2)
+        test = _fast_rows(test_rows, [(0, t0, np.ones((test_rows, 2))), (1, t1, np.ones((test_rows, 3)))],
+                          tptr, tcol)
+    return Dataset(name, train, item, test, k=64, params=dict(k=64, t=20, l=4.0, w=0.0009765625, r=-1.0))
+
+
 def kkbox_small(seed: int = 11) -> Dataset:
     """A kkbox-shaped input small enough for the fp64 oracle in a few seconds."""
     return kkbox(seed=seed, m=2000, n=3000, mean=30.0, name="kkbox_small")

@@ -41,7 +41,7 @@ def _problem():
     return ds, o
 
 
-def _partials(rank, ds, o):
+def _partials(rank, ds, o, world=WORLD):
     """This rank's partial gradients / Hv products for every half."""
     k, w, r, lam = o.k, o.omega, o.r, o.lam
     fu, f, m, n = o.fu, o.f, o.m, o.n
@@ -53,7 +53,7 @@ def _partials(rank, ds, o):
         for p in range(int(ds.train.yptr[i]), int(ds.train.yptr[i + 1])):
             Y[i, int(ds.train.ycol[p])] = 1.0
     a, b = o.get("a"), o.get("b")
-    u0, u1 = m * rank // WORLD, m * (rank + 1) // WORLD
+    u0, u1 = m * rank // world, m * (rank + 1) // world
     sh = slice(u0, u1)
     B = lambda f1, f2: O.block_index(f1, f2, f)  # noqa: E731
     P = {}
@@ -114,11 +114,11 @@ def _partials(rank, ds, o):
     return out
 
 
-def _worker(rank, port, result_path):
+def _worker(rank, port, result_path, world=WORLD):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     ds, o = _problem()
-    parts = _partials(rank, ds, o)
+    parts = _partials(rank, ds, o, world)
     worst = 0.0
     for (b12, half), (g, hv, v) in sorted(parts.items()):
         tg = torch.from_numpy(np.ascontiguousarray(g))
@@ -147,10 +147,12 @@ def _free_port():
     return p
 
 
-def test_sharded_decomposition_gloo():
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_decomposition_gloo(world):
+    # world 3: uneven user shards (40 rows: 13 / 13 / 14)
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "worst.npy")
-        mp.spawn(_worker, args=(_free_port(), path), nprocs=WORLD, join=True)
+        mp.spawn(_worker, args=(_free_port(), path, world), nprocs=world, join=True)
         worst = float(np.load(path)[0])
     assert worst < 1e-10, worst
 
@@ -171,6 +173,12 @@ def _dist_dataset(name):
         # a single item: with two ranks the second owns no item at all
         # (item-owned CG steps forced by OCFFM_ITEM_OWNED=2)
         return synth.kkbox(seed=6, m=200, n=1, mean=1.0, name="one_item")
+    if name == "uneven":
+        # 301 users and 37 items: on 3 / 4 ranks the user shards are uneven
+        # (100/100/101, 75/75/75/76) and so are the owned item chunks
+        # (ceil(37/N): 13/13/11, 10/10/10/7: the all-gather slots r >= 2 hold
+        # short chunks); the listener-id field is owned
+        return synth.kkbox(seed=9, m=301, n=37, mean=8.0, name="uneven")
     if name == "outbrain":
         # BASELINE configs[3]'s data-parallel workload at test size (SURVEY
         # §8d): fu = 2, fv = 2, k = 64, ~1 positive per row
@@ -251,6 +259,46 @@ def test_two_ranks_match_one_rank_on_gpu(name, env, monkeypatch):
         assert abs(float(r0["loss"]) - met["loss"]) <= 1e-9 * met["loss"]
         np.testing.assert_allclose(r0["ndcg"], met["ndcg"], atol=1e-12)
         np.testing.assert_allclose(r0["prec"], met["prec"], atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,name,env", [(3, "uneven", {}), (4, "uneven", {}), (4, "uneven", {"OCFFM_CCG": "2"}),
+                                            (3, "uneven", {"OCFFM_ITEM_OWNED": "0"}),
+                                            (3, "one_item", {"OCFFM_ITEM_OWNED": "2"}), (4, "outbrain", {})])
+def test_n_ranks_match_one_rank_on_gpu(world, name, env, monkeypatch):
+    """3 and 4 ranks on one device (all-reduces through the host hook):
+    uneven user shards, owned listener-id fields, item-owned CG steps whose
+    all-gather slots r >= 2 hold short chunks, ranks that own no item
+    (one_item: ranks 1.. own nothing).  fp64 within 1e-9 of one rank,
+    identical CG counts, every rank's tables."""
+    import ocffm
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_gpu_worker, args=(_free_port(), d, world, name), nprocs=world, join=True)
+        rs = [np.load(os.path.join(d, f"r{q}.npz")) for q in range(world)]
+        ds = _dist_dataset(name)
+        g = ocffm.problem_from_dataset(ds, precision=ocffm.FP64)
+        ocffm.srand(1)
+        g.init()
+        for _ in range(2):
+            g.one_epoch()
+        met = g.validate()
+        nb = g.n_blocks()
+        if name == "uneven":
+            io_on = env.get("OCFFM_ITEM_OWNED", "1") != "0"
+            assert all((int(r["io"]) > 0) == io_on for r in rs)
+            assert all(int(r["steps"]) > 0 for r in rs)  # owned listener-id halves
+        if name == "one_item":
+            assert int(rs[0]["io"]) > 0 and all(int(r["io"]) == 0 for r in rs[1:])
+        for r in rs:
+            np.testing.assert_array_equal(r["cg"], g.cg_log())
+        for idx, (what, b) in enumerate([("W", b) for b in range(nb)] + [("H", b) for b in range(nb)]):
+            ref = g.get(what, b)
+            for r in rs:
+                assert np.abs(r[f"arr_{idx}"] - ref).max() <= 1e-9 * np.abs(ref).max(), (what, b)
+        assert abs(float(rs[0]["loss"]) - met["loss"]) <= 1e-9 * met["loss"]
+        np.testing.assert_allclose(rs[0]["ndcg"], met["ndcg"], atol=1e-12)
 
 
 @pytest.mark.gpu

@@ -77,6 +77,7 @@ def parse():
                     help="N=1: also time the fp64 parity mode and the config-5 shard into 'modes'")
     ap.add_argument("--cfg5-steps", type=int, default=2, help="timed epochs of the config-5 mode (<= --steps)")
     ap.add_argument("--cfg5-rows", type=int, default=CFG5_ROWS, help="rows of the config-5 shard")
+    ap.add_argument("--cpu-all-child", type=int, default=0, help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -204,8 +205,19 @@ def run_newton(ds, prec, steps, warmup, k=32, self_side=True, world=1, rank=0, l
                 setup_s={"create": round(t_create, 3), "init": round(t_init, 3)}, io_launches=io_launches)
 
 
+T_START = time.perf_counter()
+
+
+def log(msg):
+    """Progress on stderr (a long silent run is taken for a hung one)."""
+    print(f"[bench {time.perf_counter() - T_START:6.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
+    if args.cpu_all_child:
+        _cpu_all_child(args.cpu_all_child)
+        return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -257,6 +269,7 @@ def main():
         snap["tables"] = {(w, b): g.get(w, b) for b in _blocks(fu, fv) for w in "WH"}
         snap["epoch"] = max(1, args.warmup) + 1
 
+    log(f"rank {rank}/{world}: kkbox-shape data ready, headline epochs")
     r = run_newton(ds, prec, args.steps, args.warmup, k=32, world=world, rank=rank, local=local, comm=comm,
                    allreduce=allreduce, pmc_tag="" if prec == ocffm.FP32 else "fp64_",
                    snapshot=take if want_cpu else None)
@@ -265,6 +278,7 @@ def main():
 
     cpu = None
     if want_cpu:
+        log("CPU baseline")
         cpu = cpu_baseline(ds, args.cpu_epochs, args.cpu_single_epochs, snap, r["cg_per_epoch"])
     modes = {}
     if world == 1 and args.modes == "auto":
@@ -315,6 +329,7 @@ def _blocks(fu, fv, self_side=True):
 
 def timed_mode(fn, *a):
     """A mode's result with its wall time and the process's peak host RSS."""
+    log(f"mode {fn.__name__}{'' if len(a) < 2 or not isinstance(a[-1], str) else ' ' + a[-1]}")
     t0 = time.perf_counter()
     out = fn(*a)
     out["wall_s"] = round(time.perf_counter() - t0, 1)
@@ -438,6 +453,37 @@ def _cpu_model():
     return "unknown"
 
 
+CPU_ALL_LIMIT_S = 40
+
+
+def _cpu_all_threads(threads, m):
+    """One oracle epoch of the kkbox shape from init on `threads` threads,
+    in a child process bounded by CPU_ALL_LIMIT_S seconds."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-all-child", str(threads)]
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=CPU_ALL_LIMIT_S)
+        secs = float(r.stdout.strip().splitlines()[-1])
+        return {"value": round(m / secs, 1), "cores": threads,
+                "sample": f"1 epoch from init of the same problem on {threads} threads, {secs:.2f} s"}
+    except subprocess.TimeoutExpired:
+        return {"value": None, "cores": threads, "upper_bound": round(m / CPU_ALL_LIMIT_S, 1),
+                "sample": f"1 epoch from init on {threads} threads did not finish in {CPU_ALL_LIMIT_S} s "
+                          f"(with data generation and init, {time.perf_counter() - t0:.0f} s): below "
+                          f"{m / CPU_ALL_LIMIT_S:.0f} instances/s"}
+    except Exception as e:
+        return {"value": None, "cores": threads, "sample": f"failed: {e}"}
+
+
+def _cpu_all_child(threads):
+    import oracle_lib as O
+    ds = synth.kkbox(m=ROWS_PER_GPU)
+    o = O.Oracle(ds, threads=threads, with_test=False)
+    ocffm.srand(1)
+    o.init()
+    print(o.time_epochs(1, threads), flush=True)
+
+
 def _physical_cores():
     """(physical id, core id) pairs of /proc/cpuinfo: cores, not SMT threads."""
     try:
@@ -484,12 +530,14 @@ def cpu_baseline(ds, epochs, single_epochs=1, snap=None, gpu_cg=None, all_epochs
         if gpu_cg:  # the same rate per CG step (the work an epoch does scales with its CG steps)
             out["value_at_gpu_cg_count"] = round(out["value"] * cg / gpu_cg, 1)
         # SURVEY 8(d)'s -c <all cores>: every CPU this process may run on
-        # (the box exposes the whole host; its fair share is OMP_NUM_THREADS)
+        # (the box exposes the whole host; its fair share is OMP_NUM_THREADS).
+        # The reference zeroes and sums nr_threads x D x k buffers every CG
+        # step (ffm.cpp:557,759,783-794), so its epoch grows with the thread
+        # count past a few dozen threads: the point runs in a child process
+        # under a time limit, and a timeout is reported as an upper bound.
         out["host"]["physical_cores"] = _physical_cores()
         if avail > threads and all_epochs > 0:
-            sa = o.time_epochs(all_epochs, avail)
-            out["all_threads"] = {"value": round(ds.train.m * all_epochs / sa, 1), "cores": avail,
-                                  "sample": f"{all_epochs} epoch(s) after the sample above, {sa:.2f} s"}
+            out["all_threads"] = _cpu_all_threads(avail, ds.train.m)
         if single_epochs > 0:  # also the one-thread rate (the reference's -c 1)
             s1 = o.time_epochs(single_epochs, 1)
             out["single_thread"] = {"value": round(ds.train.m * single_epochs / s1, 1), "cores": 1,

@@ -28,15 +28,25 @@ namespace ocffm {
 
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef double d2v __attribute__((ext_vector_type(2)));
+typedef double d4v __attribute__((ext_vector_type(4)));
 
+// fp64 lane width: 16 B (two doubles) or, with OCFFM_F64_WIDE, 32 B (four
+// doubles, two 16-B loads): a KP = 32 row then spans 8 lanes as in fp32, so
+// a wave walks 8 segments at once instead of 4.
+// Default wide (round 5, fp64 kkbox epoch at 10 epochs, two alternations:
+// 10.04 -> 9.50 ms; gd_cross_row 186 -> 174 us, feat_hv 1.47 -> 1.23 ms per
+// epoch); -DOCFFM_F64_WIDE=0 builds the 16-B layout.
+#ifndef OCFFM_F64_WIDE
+#define OCFFM_F64_WIDE 1
+#endif
 template <typename real> struct VT;
 template <> struct VT<float> {
   using V = f4v;
   static constexpr int N = 4;
 };
 template <> struct VT<double> {
-  using V = d2v;
-  static constexpr int N = 2;
+  using V = std::conditional_t<OCFFM_F64_WIDE != 0, d4v, d2v>;
+  static constexpr int N = OCFFM_F64_WIDE ? 4 : 2;
 };
 template <typename real> using vec_t = typename VT<real>::V;
 
@@ -62,11 +72,20 @@ constexpr int BLOCK = 256;   // 4 waves
 #ifndef OCFFM_HS_GB
 #define OCFFM_HS_GB 32  // partner-row gathers per round in k_hs_cross_seg
 #endif
+#ifndef OCFFM_HS_GB64
+// the same in its fp64 build (wide lanes: 8 gathers of 32 B per lane, 140
+// registers / 3 waves per SIMD; 16 took 202 / 2)
+#define OCFFM_HS_GB64 (OCFFM_F64_WIDE ? 8 : OCFFM_HS_GB)
+#endif
 #ifndef OCFFM_GD_OCC
-#define OCFFM_GD_OCC 1
+// fp32 k_gd_cross_seg: at least 3 waves per SIMD (with the MFMA T tile the
+// entering pass came out at 172 + 4 registers, 2 waves; bounded: 166, no spill)
+#define OCFFM_GD_OCC 3
 #endif
 #ifndef OCFFM_GD_OCC64
-#define OCFFM_GD_OCC64 OCFFM_GD_OCC  // the fp64 build of k_gd_cross_seg
+// the fp64 build of k_gd_cross_seg: wide lanes bounded to 3 waves per SIMD
+// (the entering pass: 167 registers), else the compiler's choice
+#define OCFFM_GD_OCC64 (OCFFM_F64_WIDE ? 3 : 1)
 #endif
 #ifndef OCFFM_GD_GB64
 // fp64: 4 gathers per round (3 / 4 waves per SIMD instead of 2 / 3; the
@@ -242,8 +261,26 @@ __device__ __forceinline__ BufView buf_view(const void *p, uint64_t bytes) {
                  (uint32_t)bytes};
 }
 template <typename real> __device__ __forceinline__ vec_t<real> bld(const BufView &b, uint32_t off) {
-  return __builtin_bit_cast(vec_t<real>, __builtin_amdgcn_raw_buffer_load_b128(b.r, off, 0, 0));
+  if constexpr (sizeof(vec_t<real>) == 16) {
+    return __builtin_bit_cast(vec_t<real>, __builtin_amdgcn_raw_buffer_load_b128(b.r, off, 0, 0));
+  } else {  // a 32-B lane: two 16-B loads (an out-of-range offset reads zero for both)
+    const d2v lo = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(b.r, off, 0, 0));
+    const d2v hi = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(b.r, off == b.oob ? off : off + 16u, 0, 0));
+    return vec_t<real>{lo[0], lo[1], hi[0], hi[1]};
+  }
 }
+// the same with the sc1 bit (aux 16: the last-arriver hand-off's loads)
+template <typename real> __device__ __forceinline__ vec_t<real> bld_sc1(const BufView &b, uint32_t off) {
+  if constexpr (sizeof(vec_t<real>) == 16) {
+    return __builtin_bit_cast(vec_t<real>, __builtin_amdgcn_raw_buffer_load_b128(b.r, off, 0, 16));
+  } else {
+    const d2v lo = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(b.r, off, 0, 16));
+    const d2v hi = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(b.r, off == b.oob ? off : off + 16u, 0, 16));
+    return vec_t<real>{lo[0], lo[1], hi[0], hi[1]};
+  }
+}
+// bytes of one lane's share of a row (16, or 32 for wide fp64 lanes)
+template <typename real> constexpr uint32_t LANE_B = (uint32_t)sizeof(vec_t<real>);
 template <typename real> __device__ __forceinline__ real bld1(const BufView &b, uint32_t off);
 template <> __device__ __forceinline__ float bld1<float>(const BufView &b, uint32_t off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(b.r, off, 0, 0));
@@ -360,7 +397,7 @@ template <typename real, int KP, int GB_ = 8> struct PosPass {
     }
   }
   static __device__ __forceinline__ uint32_t row_off(uint32_t j, const BufView &b, int li) {
-    return j == POS_NONE ? b.oob : j * ROWB + (uint32_t)li * 16u;
+    return j == POS_NONE ? b.oob : j * ROWB + (uint32_t)li * LANE_B<real>;
   }
 };
 
@@ -430,6 +467,9 @@ __device__ __forceinline__ bool last_block(const double (&v)[NV], double *part, 
     int last = 0;
     if (__hip_atomic_fetch_add(sub, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1) {
       __hip_atomic_store(sub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // the reset lands before the top ticket (a persistent grid's next
+      // round takes tickets on the same words right after the release)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned groups = gridDim.x < (unsigned)TICK_SUB ? gridDim.x : (unsigned)TICK_SUB;
       last = __hip_atomic_fetch_add(tick, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == groups - 1;
     }
@@ -907,6 +947,145 @@ __global__ __launch_bounds__(TBLOCK) void k_rows_T(uint64_t R, int C, const floa
 // (gd_cross row body, ffm.cpp:658-700); y~ = base + a_i + b_j.  M in LDS.
 enum { BM_FULL = 0, BM_IN = 1, BM_ENTER = 2 };  // base modes of k_gd_cross_seg
 
+// T_i = sum_c P_c[i] M_c of the cross gradient (ffm.cpp:663-670) on the
+// matrix cores, inside k_gd_cross_seg (round 5).  A block iteration covers
+// SB = 4 NSG consecutive segments; T of their rows (first segments only:
+// the others carry no row term) is the (SB x C KP) x (C KP x KP) product
+// [P_1 .. P_C]_rows [M_1; ..; M_C], cut into 16 x 16 tiles, one per wave
+// (fp32: SB KP = 1024, four tiles; fp64 at KP = 32: two, waves 2, 3 idle),
+// each the chain of C KP / 4 v_mfma_{f32,f64}_16x16x4 over the whole K.
+// The K order inside each chunk of 16 is permuted so that lane l (row l%16,
+// k-group q = l/16) loads its 4 A values as one 16-B (fp64: 32-B) row slice
+// A[row][16 j + 4 q .. +3] and takes them as the K values of 4 consecutive
+// MFMAs; M is staged in LDS in the matching order Bt[(k/4) KP + n][k%4], so
+// the 4 B values are one 16-B (32-B) LDS read.  The tile goes to LDS (Tl)
+// and each segment's subgroup reads its row back.  The VALU version read M
+// from LDS once per row and table (32 ds_read_b128 per row and table at KP =
+// 32): LDS-bound at ~4x the VALU time on the song-id item halves.
+#ifndef OCFFM_NO_TMMA
+#define OCFFM_NO_TMMA 0  // experiment builds: -DOCFFM_NO_TMMA=1 keeps T_i on the VALU
+#endif
+template <typename real, int KP> struct TMma {
+  using G = Geo<real, KP>;
+  static constexpr bool OK =
+      !OCFFM_NO_TMMA && ((std::is_same<real, float>::value && (KP == 16 || KP == 32 || KP == 64)) ||
+                         (std::is_same<real, double>::value && KP == 32));
+  static constexpr int SB = 4 * G::NSG;                    // segments (tile rows) per block iteration
+  static constexpr int TR = SB >= 16 ? SB / 16 : 1, TC = KP >= 16 ? KP / 16 : 1;
+  static constexpr int NTW = TR * TC;                     // waves computing a tile
+  // LDS bytes beyond M (the T tile)
+  static constexpr size_t tile_bytes() { return (size_t)SB * KP * sizeof(real); }
+  // output row of D register r in lane l (v_mfma_f32_16x16x4f32: lane group
+  // l/16 holds 4 consecutive rows; v_mfma_f64_16x16x4f64: rows l/16 + 4 r,
+  // k_gram_mfma_f64's layout)
+  static __device__ __forceinline__ int drow(int l, int r) {
+    if constexpr (std::is_same<real, float>::value) return 4 * (l >> 4) + r;
+    else return (l >> 4) + 4 * r;
+  }
+  // M (C KP x KP row-major, c-major) -> Bt in LDS
+  static __device__ __forceinline__ void stage(const real *__restrict__ M, int C, real *Bt) {
+    const int tot = C * KP * KP;
+    for (int t = threadIdx.x; t < tot; t += BLOCK) {
+      const int k = t / KP, n = t % KP;
+      Bt[((k >> 2) * KP + n) * 4 + (k & 3)] = M[t];
+    }
+  }
+  // the tile of wave w (< NTW) for segments [base, base + SB) into Tl
+  static __device__ __forceinline__ void tile(uint64_t base, uint64_t nseg, const Seg *__restrict__ segs, int C,
+                                              const real *const *__restrict__ Ptabs, const real *Bt, real *Tl,
+                                              int w, int lane) {
+    const int tr = w % TR, tc = w / TR;
+    const int m = lane & 15, q = lane >> 4;
+    const uint64_t si = base + (uint64_t)tr * 16 + m;
+    bool have = false;
+    uint64_t row = 0;
+    if (si < nseg) {
+      const Seg s = segs[si];
+      have = seg_first(s);
+      row = s.row;
+    }
+    const int nch = C * KP / 16;
+    if constexpr (std::is_same<real, float>::value) {
+      f4v acc = {0.f, 0.f, 0.f, 0.f};
+      constexpr int GR = 4;  // chunks per load group (two groups in flight)
+      f4v a[2][GR];
+      auto load = [&](auto SB_, int j0) {
+        constexpr int sb = decltype(SB_)::value;
+#pragma unroll
+        for (int u = 0; u < GR; u++) {
+          const int j = j0 + u, k0 = 16 * j;
+          a[sb][u] = (have && j < nch) ? gvld<float>(Ptabs[k0 / KP] + row * KP + (k0 % KP) + 4 * q)
+                                       : f4v{0.f, 0.f, 0.f, 0.f};
+        }
+      };
+      auto mma = [&](auto SB_, int j0) {
+        constexpr int sb = decltype(SB_)::value;
+#pragma unroll
+        for (int u = 0; u < GR; u++) {
+          const int j = j0 + u;
+          if (j < nch) {
+            const f4v b = *reinterpret_cast<const f4v *>(Bt + ((4 * j + q) * KP + tc * 16 + m) * 4);
+#pragma unroll
+            for (int s = 0; s < 4; s++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[sb][u][s], b[s], acc, 0, 0, 0);
+          }
+        }
+      };
+      load(std::integral_constant<int, 0>(), 0);
+      for (int j0 = 0; j0 < nch; j0 += 2 * GR) {
+        load(std::integral_constant<int, 1>(), j0 + GR);
+        mma(std::integral_constant<int, 0>(), j0);
+        if (j0 + GR >= nch) break;
+        load(std::integral_constant<int, 0>(), j0 + 2 * GR);
+        mma(std::integral_constant<int, 1>(), j0 + GR);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++) Tl[(tr * 16 + drow(lane, r)) * KP + tc * 16 + m] = acc[r];
+    } else {
+      typedef double d4 __attribute__((ext_vector_type(4)));
+      d4 acc = {0.0, 0.0, 0.0, 0.0};
+      constexpr int GR = 2;
+      d2v a[2][GR][2];
+      auto load = [&](auto SB_, int j0) {
+        constexpr int sb = decltype(SB_)::value;
+#pragma unroll
+        for (int u = 0; u < GR; u++) {
+          const int j = j0 + u, k0 = 16 * j;
+          const bool ok = have && j < nch;
+          const double *p = ok ? Ptabs[k0 / KP] + row * KP + (k0 % KP) + 4 * q : nullptr;
+#pragma unroll
+          for (int h = 0; h < 2; h++)
+            a[sb][u][h] = ok ? *(const __attribute__((address_space(1))) d2v *)(p + 2 * h) : d2v{0.0, 0.0};
+        }
+      };
+      auto mma = [&](auto SB_, int j0) {
+        constexpr int sb = decltype(SB_)::value;
+#pragma unroll
+        for (int u = 0; u < GR; u++) {
+          const int j = j0 + u;
+          if (j < nch) {
+            const double *bp = Bt + ((4 * j + q) * KP + tc * 16 + m) * 4;
+            const d2v b0 = *reinterpret_cast<const d2v *>(bp), b1 = *reinterpret_cast<const d2v *>(bp + 2);
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[sb][u][0][0], b0[0], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[sb][u][0][1], b0[1], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[sb][u][1][0], b1[0], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[sb][u][1][1], b1[1], acc, 0, 0, 0);
+          }
+        }
+      };
+      load(std::integral_constant<int, 0>(), 0);
+      for (int j0 = 0; j0 < nch; j0 += 2 * GR) {
+        load(std::integral_constant<int, 1>(), j0 + GR);
+        mma(std::integral_constant<int, 0>(), j0);
+        if (j0 + GR >= nch) break;
+        load(std::integral_constant<int, 0>(), j0 + 2 * GR);
+        mma(std::integral_constant<int, 1>(), j0 + GR);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++) Tl[(tr * 16 + drow(lane, r)) * KP + tc * 16 + m] = acc[r];
+    }
+  }
+};
+
 template <typename real, int KP, bool MLDS, int BM, bool TP = false>
 __global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_GD_OCC64 : OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                         const uint32_t *__restrict__ ycol,
@@ -932,9 +1111,16 @@ __global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_GD_OCC64 : OCFFM_G
   extern __shared__ __align__(16) unsigned char smem_raw[];
   real *Ms = reinterpret_cast<real *>(smem_raw);
   const real *Mp = M;
+  // TM: T_i on the matrix cores, a tile per block iteration (TMma); else
   // TL: T_i by lane-local accumulation over transposed M (fp32, KP <= 32)
-  constexpr bool TL = MLDS && std::is_same<real, float>::value && KP <= 32;
-  if (MLDS && !TP) {
+  using TMM = TMma<real, KP>;
+  constexpr bool TM = MLDS && !TP && TMM::OK;
+  constexpr bool TL = !TM && MLDS && std::is_same<real, float>::value && KP <= 32;
+  real *Tl = Ms + (TM ? (size_t)C * KP * KP : 0);
+  if (TM) {
+    TMM::stage(M, C, Ms);
+    __syncthreads();
+  } else if (MLDS && !TP) {
     const int tot = C * KP * KP;
     for (int t = threadIdx.x; t < tot; t += BLOCK) {
       if constexpr (TL) {  // pair-transposed (lane_vecmat_acc)
@@ -1028,7 +1214,12 @@ __global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_GD_OCC64 : OCFFM_G
       const real z = ai - (real)r;
       pk += vsplat<real>((real)w) * (vld<real>(Tpre + i * KP + li * G::VE) + vsplat<real>(z) * oQ + bQ);
     }
-    if (!TP && seg_first(sgm)) {
+    if (TM && seg_first(sgm)) {  // T_i from the block's MFMA tile
+      const real z = ai - (real)r;
+      const vec_t<real> t = vld<real>(Tl + (size_t)((threadIdx.x >> 6) * G::NSG + sg) * KP + li * G::VE);
+      pk += vsplat<real>((real)w) * (t + vsplat<real>(z) * oQ + bQ);
+    }
+    if (!TP && !TM && seg_first(sgm)) {
       // T_i: the C row loads are independent; issue them in batches so the
       // vector-matrix products do not wait on one HBM round trip per table
       constexpr int CB = 4;
@@ -1064,7 +1255,21 @@ __global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_GD_OCC64 : OCFFM_G
     }
     return pk;
   };
-  for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) vst<real>(h + s * KP + li * G::VE, body(segs[s]));
+  if constexpr (TM) {
+    // block iterations over SB consecutive segments: the waves' MFMA tile,
+    // a barrier, the segments (each reads its row of the tile), a barrier
+    // before the next iteration rewrites the tile
+    const int wv = threadIdx.x >> 6;
+    for (uint64_t base = (uint64_t)blockIdx.x * TMM::SB; base < nseg; base += (uint64_t)gridDim.x * TMM::SB) {
+      if (wv < TMM::NTW) TMM::tile(base, nseg, segs, C, Ptabs, Ms, Tl, wv, lane);
+      __syncthreads();
+      const uint64_t s = base + (uint64_t)wv * G::NSG + sg;
+      if (s < nseg) vst<real>(h + s * KP + li * G::VE, body(segs[s]));
+      __syncthreads();
+    }
+  } else {
+    for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) vst<real>(h + s * KP + li * G::VE, body(segs[s]));
+  }
 }
 
 // Per segment s: ysum[s] = sum_{p in seg} (base_p + b1[ycol_p]).  A side's
@@ -1761,6 +1966,90 @@ __global__ __launch_bounds__(BLOCK) void k_hv_cgram(uint64_t D, const real *__re
   if constexpr (MODE != 2) fin_blocks<real, 1>(f, dsum);
 }
 
+// ------------------------------------------ persistent column-Gram CG ---
+// Every CG step of a half whose Hessian-vector product is the D column
+// Grams (k_hv_cgram: the genre / artist side halves, the column-Gram cross
+// halves; ffm.cpp:761-812) in ONE launch (round 5, OCFFM_CGP): a step is
+// each column's s = G_c p_c and its finalisation by the column's fixed
+// owner (so no vector crosses a block), the grid's dot products by the
+// last-arriving block (last_block), which publishes alpha, beta and the
+// verdict (the same arithmetic as cg_publish, through agent-scope stores)
+// and then releases the grid through a generation word that the other
+// blocks poll (bounded spin); the next step reads the scalars with
+// agent-scope loads.  The grid must be co-resident (host: at most one
+// block per CU).  No host round trip or kernel boundary between steps.
+__device__ __forceinline__ double ald(const double *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ald(const int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void ast(double *p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ast(int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+constexpr unsigned CGP_SPIN_MAX = 1u << 24;  // ~seconds of s_sleep 1: a stuck grid gives up (err) instead of hanging
+template <typename real, int KP>
+__global__ __launch_bounds__(BLOCK) void k_cg_cgram(uint64_t D, const real *__restrict__ G, Fin<real> f,
+                                                    unsigned *__restrict__ gen, unsigned gen0, int *__restrict__ err) {
+  using Gm = Geo<real, KP>;
+  WAVE_SETUP
+  const int sg = lane / Gm::LPR, li = lane % Gm::LPR;
+  CgState *st = f.st;
+  __shared__ int s_ok;
+  for (int it = 1; it <= MAXCG; it++) {
+    if (!ald(&st->run[it])) return;  // the same word for every block (read after the barrier)
+    const bool upd = it > 1;
+    const real alpha = upd ? (real)ald(&st->alpha) : (real)0, beta = upd ? (real)ald(&st->beta) : (real)0;
+    f.it = it;
+    double dsum[3] = {0, 0, 0};
+    for (uint64_t c = wave * Gm::NSG + sg; c < D; c += nwaves * Gm::NSG) {
+      const FinOps<real> ops = fin_load<real, KP, 1>(f, (uint32_t)c, upd, li);
+      vec_t<real> pt = ops.w_or_p;
+      if (upd) pt = (ops.r - vsplat<real>(alpha) * ops.hp) + vsplat<real>(beta) * ops.w_or_p;
+      vec_t<real> s;
+      if constexpr (KP >= 64) s = sg_vecmat_rolled<real, KP, 4>(pt, G + c * KP * KP, li);
+      else s = sg_vecmat<real, KP>(pt, G + c * KP * KP, li);
+      col_finalize<real, KP, 1>(f, (uint32_t)c, s, alpha, beta, upd, li, dsum, ops);
+    }
+    double bv[3] = {block_sum(dsum[0]), block_sum(dsum[1]), block_sum(dsum[2])}, tot[3];
+    if (last_block<3>(bv, f.part, f.tick, tot)) {
+      if (threadIdx.x == 0) {
+        // cg_publish MODE 1 (ffm.cpp:803-809) through agent-scope stores
+        const double r2 = ald(&st->r2), g2 = ald(&st->g2);
+        const double a = r2 / tot[0];
+        const double r2n = r2 - 2 * a * tot[1] + a * a * tot[2];
+        ast(&st->vhv, tot[0]);
+        ast(&st->alpha, a);
+        ast(&st->beta, r2n / r2);
+        ast(&st->r2, r2n);
+        ast(&st->nr_cg, it);
+        const int go = (it < MAXCG && g2 * CG_EPS < r2n) ? 1 : 0;
+        ast(&st->run[it + 1], go);
+        if (f.run_host)
+          __hip_atomic_store(f.run_host + it + 1, go ? RUN_GO : RUN_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store above (and the tickets' reset) landed
+        __hip_atomic_store(gen, gen0 + (unsigned)it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+    } else {
+      if (threadIdx.x == 0) {
+        int ok = 1;
+        unsigned spins = 0;
+        while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen0 + (unsigned)it) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > CGP_SPIN_MAX) {
+            ok = 0;
+            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+        }
+        s_ok = ok;
+      }
+      __syncthreads();
+      if (!s_ok) return;
+    }
+  }
+}
+
 // Per segment of row i: h[s] = (1-w) sum_{j in seg} <phi_i, q_j> q_j
 // + [first] w phi_i QTQ, phi_i = X_i p  (hs_cross row body, ffm.cpp:715-738;
 // tau = X_i (V QTQ) = phi_i QTQ).  QTQ staged in LDS; phi_i's components
@@ -1780,7 +2069,8 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
                                                         const uint32_t *__restrict__ hot_seg,
                                                         const real *__restrict__ hotG) {
   using G = Geo<real, KP>;
-  using PP = PosPass<real, KP, OCFFM_HS_GB>;  // gathers per round (32: one round per <= 32-positive segment)
+  // gathers per round (32: one round per <= 32-positive segment)
+  using PP = PosPass<real, KP, sizeof(real) == 8 ? OCFFM_HS_GB64 : OCFFM_HS_GB>;
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real));
   if (run && !*run) return;
   const bool upd = st && it > 1;
@@ -1930,7 +2220,7 @@ __global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__res
         constexpr int e = decltype(E)::value;
         const uint32_t r = sg_bcast<G::LPR, e % G::LPR>(rr[e / G::LPR], li);
         const real x = sg_bcast<G::LPR, e % G::LPR>(vv[e / G::LPR], li);
-        const uint32_t off = b0 + e < jb.e ? r * (uint32_t)(KP * sizeof(real)) + li * 16u : hb.oob;
+        const uint32_t off = b0 + e < jb.e ? r * (uint32_t)(KP * sizeof(real)) + li * LANE_B<real> : hb.oob;
         hv[e] = vsplat<real>(x) * bld<real>(hb, off);
       });
 #pragma unroll
@@ -1969,7 +2259,7 @@ __global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__res
             for (int u = 0; u < RB; u++) {
               const uint32_t q = q0 + u * G::NSG;
               const uint32_t off = q < jb.nparts ? (uint32_t)(((size_t)(s0 + q) * KP + li * G::VE) * sizeof(real)) : pv.oob;
-              y[u] = __builtin_bit_cast(vec_t<real>, __builtin_amdgcn_raw_buffer_load_b128(pv.r, off, 0, 16));
+              y[u] = bld_sc1<real>(pv, off);
             }
 #pragma unroll
             for (int u = 0; u < RB; u++) a += y[u];

@@ -435,7 +435,16 @@ template <typename real> class Problem final : public ProblemBase {
     part_.alloc(1 << 22, false);
     st_.alloc(1);
     tabs_.alloc(4 * std::max<uint32_t>(C_, 1) + 4);
-    HIPCHK(hipHostMalloc((void **)&run_host_, sizeof(int) * (MAXCG + 2), hipHostMallocMapped | hipHostMallocCoherent));
+    // (MAXCG + 2 verdict words, then the persistent CG's error word at MAXCG + 3)
+    HIPCHK(hipHostMalloc((void **)&run_host_, sizeof(int) * (MAXCG + 4), hipHostMallocMapped | hipHostMallocCoherent));
+    run_host_[MAXCG + 3] = 0;
+    {
+      int dev = 0, ncu = 0;
+      HIPCHK(hipGetDevice(&dev));
+      HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+      ncu_ = (unsigned)std::max(1, ncu);
+    }
+    cgp_gen_buf_.alloc(1);
     std::memset(run_host_, 0, sizeof(int) * (MAXCG + 2));
     HIPCHK(hipHostGetDevicePointer((void **)&run_host_dev_, run_host_, 0));
     if (comm_.host_fn) HIPCHK(hipHostMalloc((void **)&stage_, Dmax * kp_ * sizeof(real), hipHostMallocDefault));
@@ -1905,8 +1914,10 @@ template <typename real> class Problem final : public ProblemBase {
           constexpr int BM = decltype(bm)::value;
           auto go3 = [&](auto tpc) {
             constexpr bool TP = decltype(tpc)::value;
+            // (with T on the matrix cores the block also holds its T tile)
+            constexpr bool TM = ML && !TP && TMma<real, KP>::OK;
             launch(k_gd_cross_seg<real, KP, ML, BM, TP>, grid_for(own.nseg, 4 * Gm::NSG, gd_blocks_), BLOCK,
-                TP ? 0 : (ML ? msz : 0), own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
+                TP ? 0 : (ML ? msz + (TM ? TMma<real, KP>::tile_bytes() : 0) : 0), own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
                 (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, h.partner->bias.p, w_,
                 r_, h_.p, (uint64_t)h.partner->R, cur, drow, dxs, (const uint32_t *)own.perm.p,
                 TP ? (const real *)Tpre_.p : (const real *)nullptr,
@@ -1966,7 +1977,7 @@ template <typename real> class Problem final : public ProblemBase {
   }
 
   // subgroups per wave of this problem's row geometry (kernels.hpp: Geo)
-  int nsg() const { return 64 / std::max<int>(1, (int)(kp_ * sizeof(real) / 16)); }
+  int nsg() const { return 64 / std::max<int>(1, (int)(kp_ / VT<real>::N)); }
 
   // Restore the full base from the block-excluded y~:
   // base_ij = e_ij + <P_b[i], Q_b[j]> - a_i - b_j in the user orientation
@@ -2526,7 +2537,7 @@ template <typename real> class Problem final : public ProblemBase {
     hv_product(h, it);
     if (!exact_r2(h)) return;
     const Fin<real> fin = make_fin(h, it);
-    const uint64_t nv = h.D * kp_ / (16 / sizeof(real));
+    const uint64_t nv = h.D * kp_ / VT<real>::N;
     prof_launch("cg_r2", (double)h.D * kp_ * sizeof(real) * 2,
                 [&] { launch(k_cg_r2<real>, grid_for(nv, BLOCK, 1024), BLOCK, 0, nv, fin); });
   }
@@ -2733,6 +2744,30 @@ template <typename real> class Problem final : public ProblemBase {
     });
   }
 
+  // Persistent column-Gram CG (k_cg_cgram): one GPU (or a replicated half:
+  // no collective inside), the plain expanded residual, not item-owned.
+  bool cgp_ok(const HalfCtx &h) const {
+    return cgp_on_ && cgram(h) && (!comm_.active() || repl(h)) && !exact_r2(h) && !io_half(h) && h.D > 0;
+  }
+  double cgp_step_bytes(const HalfCtx &h) const {
+    return (double)h.D * kp_ * kp_ * sizeof(real) + (double)h.D * kp_ * sizeof(real) * 9;
+  }
+  void cg_persist(HalfCtx &h) {
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      using Gm = Geo<real, KP>;
+      const Fin<real> fin = make_fin(h, 1);
+      // co-resident grid: at most one block per CU
+      const unsigned grid = (unsigned)std::min<uint64_t>((h.D + 4 * Gm::NSG - 1) / (4 * Gm::NSG), ncu_);
+      const unsigned g0 = cgp_gen_;
+      cgp_gen_ += MAXCG + 1;
+      prof_launch("cg_cgram", 0.0, [&] {
+        launch(k_cg_cgram<real, KP>, grid, BLOCK, 0, (uint64_t)h.D, gram_of(h), fin, cgp_gen_buf_.p, g0,
+               run_host_dev_ + MAXCG + 3);
+      });
+    });
+  }
+
   void hv_product(HalfCtx &h, int it) {
     DevSide<real> &own = *h.own;
     const int *run = &st_.p->run[it];
@@ -2875,6 +2910,24 @@ template <typename real> class Problem final : public ProblemBase {
     col_grams(h);
     hot_grams(h);
     if (io) io_begin(h);
+    if (cgp_ok(h)) {
+      // the whole CG in one persistent launch, the update queued right
+      // behind it (no speculation, no host round trip inside the half)
+      prof_tag_ = 1;
+      cg_persist(h);
+      prof_tag_ = 0;
+      finish_half(h, nullptr);
+      queued = true;
+      examine(MAXCG);
+      if (run_host_[MAXCG + 3]) {
+        run_host_[MAXCG + 3] = 0;
+        throw Error(OCFFM_E_HIP, "persistent CG grid did not complete (k_cg_cgram spin limit)");
+      }
+      if (profiling && pending_.size() > pend0) {  // its bytes: the steps that ran
+        for (size_t q = pend0; q < pending_.size(); q++)
+          if (pending_[q].name == "cg_cgram") pending_[q].bytes = (double)nr * cgp_step_bytes(h);
+      }
+    }
     for (int it = 1; it <= MAXCG && !done && !queued; it++) {
       prof_tag_ = it;
       hv_pass(h, it);
@@ -3117,6 +3170,11 @@ template <typename real> class Problem final : public ProblemBase {
   DevBuf<CgState> st_;
   DevBuf<real *> tabs_;
   int *run_host_ = nullptr, *run_host_dev_ = nullptr;
+  // persistent column-Gram CG (k_cg_cgram, OCFFM_CGP): the grid's release
+  // word (monotonic across launches), the CU count that bounds its grid
+  DevBuf<unsigned> cgp_gen_buf_;
+  unsigned cgp_gen_ = 0, ncu_ = 256;
+  bool cgp_on_ = !std::getenv("OCFFM_CGP") || std::atoi(std::getenv("OCFFM_CGP")) != 0;
   real *stage_ = nullptr;
   static constexpr uint64_t DSTAGE = 64;
   double *dstage_ = nullptr;  // host all-reduce stage of the owned-field dot products

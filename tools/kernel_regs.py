@@ -7,7 +7,7 @@ import sys
 import tempfile
 
 LLVM = "/opt/rocm/lib/llvm/bin"
-LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "one-class-ffm_amd", "libocffm.so")
+LIB = os.environ.get("OCFFM_LIB") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "one-class-ffm_amd", "libocffm.so")
 
 
 def main():

@@ -946,6 +946,14 @@ __global__ __launch_bounds__(TBLOCK) void k_rows_T(uint64_t R, int C, const floa
 //          + [first] w (T_i + (a_i - r) oQ + bQ),   T_i = sum_c P_c[i] M_c
 // (gd_cross row body, ffm.cpp:658-700); y~ = base + a_i + b_j.  M in LDS.
 enum { BM_FULL = 0, BM_IN = 1, BM_ENTER = 2 };  // base modes of k_gd_cross_seg
+// Experiment builds: -DOCFFM_GD_PROBE=1 launches, ahead of every cross
+// gradient pass, its PRB instantiation ("gd_probe"): the same loads (the
+// positions, the stored values and the partner-row gathers of every
+// position, one or two per position) without the arithmetic, the T_i term
+// and the stored-value writes: the time of its gathers alone.
+#ifndef OCFFM_GD_PROBE
+#define OCFFM_GD_PROBE 0
+#endif
 
 // T_i = sum_c P_c[i] M_c of the cross gradient (ffm.cpp:663-670) on the
 // matrix cores, inside k_gd_cross_seg (round 5).  A block iteration covers
@@ -1086,7 +1094,7 @@ template <typename real, int KP> struct TMma {
   }
 };
 
-template <typename real, int KP, bool MLDS, int BM, bool TP = false>
+template <typename real, int KP, bool MLDS, int BM, bool TP = false, bool PRB = false>
 __global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_GD_OCC64 : OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                         const uint32_t *__restrict__ ycol,
                                                         real *__restrict__ yt, const real *__restrict__ Q1,
@@ -1187,6 +1195,14 @@ __global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_GD_OCC64 : OCFFM_G
             if (dxs) xv[u] = bld<real>(xb, PP::row_off(j, xb, li));
           }
         });
+        if constexpr (PRB) {  // bound probe: the gathers and the sum, no dot products
+#pragma unroll
+          for (int u = 0; u < PP::GB; u++) {
+            pk += qv[u];
+            if constexpr (WR) pk += xv[u];
+          }
+          return;
+        }
         if constexpr (BM != BM_FULL) {
 #pragma unroll
           for (int u = 0; u < PP::GB; u++) {
@@ -1202,7 +1218,7 @@ __global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_GD_OCC64 : OCFFM_G
 #pragma unroll
         for (int u = 0; u < PP::GB; u++) pk += vsplat<real>(cpos * yb[u] - cneg) * qv[u];
       });
-      if constexpr (WR) {
+      if constexpr (WR && !PRB) {
 #pragma unroll
         for (int t = 0; t < PP::UT; t++) {
           const int64_t q = p0 + li + t * G::LPR;
@@ -1210,16 +1226,16 @@ __global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_GD_OCC64 : OCFFM_G
         }
       }
     }
-    if (TP && seg_first(sgm)) {
+    if (!PRB && TP && seg_first(sgm)) {
       const real z = ai - (real)r;
       pk += vsplat<real>((real)w) * (vld<real>(Tpre + i * KP + li * G::VE) + vsplat<real>(z) * oQ + bQ);
     }
-    if (TM && seg_first(sgm)) {  // T_i from the block's MFMA tile
+    if (!PRB && TM && seg_first(sgm)) {  // T_i from the block's MFMA tile
       const real z = ai - (real)r;
       const vec_t<real> t = vld<real>(Tl + (size_t)((threadIdx.x >> 6) * G::NSG + sg) * KP + li * G::VE);
       pk += vsplat<real>((real)w) * (t + vsplat<real>(z) * oQ + bQ);
     }
-    if (!TP && !TM && seg_first(sgm)) {
+    if (!PRB && !TP && !TM && seg_first(sgm)) {
       // T_i: the C row loads are independent; issue them in batches so the
       // vector-matrix products do not wait on one HBM round trip per table
       constexpr int CB = 4;
@@ -1261,7 +1277,7 @@ __global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_GD_OCC64 : OCFFM_G
     // before the next iteration rewrites the tile
     const int wv = threadIdx.x >> 6;
     for (uint64_t base = (uint64_t)blockIdx.x * TMM::SB; base < nseg; base += (uint64_t)gridDim.x * TMM::SB) {
-      if (wv < TMM::NTW) TMM::tile(base, nseg, segs, C, Ptabs, Ms, Tl, wv, lane);
+      if (!PRB && wv < TMM::NTW) TMM::tile(base, nseg, segs, C, Ptabs, Ms, Tl, wv, lane);
       __syncthreads();
       const uint64_t s = base + (uint64_t)wv * G::NSG + sg;
       if (s < nseg) vst<real>(h + s * KP + li * G::VE, body(segs[s]));
@@ -1441,7 +1457,7 @@ __global__ __launch_bounds__(BLOCK) void k_col_gram(const Job *__restrict__ chun
                                                     const real *__restrict__ cval, const int64_t *__restrict__ yptr,
                                                     const real *__restrict__ Q1, double w, double n1,
                                                     real *__restrict__ G, real *__restrict__ gpart,
-                                                    unsigned *__restrict__ cnt) {
+                                                    unsigned *__restrict__ cnt, int pw) {
   constexpr int CH = cgram_rows(KP, (int)sizeof(real));
   constexpr int KK = KP * KP;
   constexpr int NE = (KK + BLOCK - 1) / BLOCK;
@@ -1454,7 +1470,7 @@ __global__ __launch_bounds__(BLOCK) void k_col_gram(const Job *__restrict__ chun
   for (int r = threadIdx.x; r < n; r += BLOCK) {
     const uint32_t i = crow[jb.b + r];
     const real x = cval[jb.b + r];
-    cs[r] = (real)((1 - w) * (double)(yptr[i + 1] - yptr[i]) + w * n1) * x * x;
+    cs[r] = (real)((1 - w) * (double)(yptr[i + 1] - yptr[i]) + w * n1) * (pw ? x : x * x);
   }
   __syncthreads();
   real acc[NE];
@@ -1542,7 +1558,7 @@ static __global__ __launch_bounds__(BLOCK) void k_col_gram32(uint64_t nchunks, c
                                                       const uint32_t *__restrict__ crow,
                                                       const float *__restrict__ cval, const int64_t *__restrict__ yptr,
                                                       const float *__restrict__ Q1, uint64_t q1rows, double w, double n1,
-                                                      float *__restrict__ G, float *__restrict__ gpart) {
+                                                      float *__restrict__ G, float *__restrict__ gpart, int pw) {
   typedef float f16x __attribute__((ext_vector_type(16)));
   const int lane = threadIdx.x & 63;
   const uint64_t wv = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
@@ -1554,7 +1570,7 @@ static __global__ __launch_bounds__(BLOCK) void k_col_gram32(uint64_t nchunks, c
   if (lane < n) {
     il = crow[jb.b + lane];
     const float x = cval[jb.b + lane];
-    cl = (float)((1 - w) * (double)(yptr[il + 1] - yptr[il]) + w * n1) * x * x;
+    cl = (float)((1 - w) * (double)(yptr[il + 1] - yptr[il]) + w * n1) * (pw ? x : x * x);
   }
   const BufView qb = buf_view(Q1, q1rows * 128);
   const int e = lane & 31, hf = lane >> 5;
@@ -1589,7 +1605,7 @@ static __global__ __launch_bounds__(BLOCK) void k_col_gram_f64(uint64_t nchunks,
                                                               const int64_t *__restrict__ yptr,
                                                               const double *__restrict__ Q1, uint64_t q1rows, double w,
                                                               double n1, double *__restrict__ G,
-                                                              double *__restrict__ gpart) {
+                                                              double *__restrict__ gpart, int pw) {
   typedef double d4 __attribute__((ext_vector_type(4)));
   constexpr int NG = CGRAM32_ROWS / 4;
   const int lane = threadIdx.x & 63;
@@ -1602,7 +1618,7 @@ static __global__ __launch_bounds__(BLOCK) void k_col_gram_f64(uint64_t nchunks,
   if (lane < n) {
     il = crow[jb.b + lane];
     const double x = cval[jb.b + lane];
-    cl = ((1 - w) * (double)(yptr[il + 1] - yptr[il]) + w * n1) * x * x;
+    cl = ((1 - w) * (double)(yptr[il + 1] - yptr[il]) + w * n1) * (pw ? x : x * x);
   }
   const BufView qb = buf_view(Q1, q1rows * 256);
   const int c16 = lane & 15, rq = lane >> 4;
@@ -1966,6 +1982,94 @@ __global__ __launch_bounds__(BLOCK) void k_hv_cgram(uint64_t D, const real *__re
   if constexpr (MODE != 2) fin_blocks<real, 1>(f, dsum);
 }
 
+// ------------------------------------------------------- pair Grams ---
+// Side halves of a low-cardinality field with several nodes per row (the
+// kkbox context field: 120 features, two per row; round 5, OCFFM_PGRAM).
+// The field block of the side Hessian (hs_side, ffm.cpp:594-628) is
+//   (H v)_a = sum_b G_ab v_b,  G_ab = sum_{i: X_ia X_ib != 0} d_i X_ia X_ib q_i q_i^T,
+// one k x k Gram per feature pair (a <= b) present in some row, built once
+// per half (k_col_gram* with pair weights).  A CG step is then ONE launch
+// instead of the row pass over every row plus a feature pass whose heavy
+// columns (~500 rows each) cost a chain of dependent rounds (~21 us per
+// step): block a sums G_ab p_b over feature a's pairs (its subgroups split
+// the adjacency list, p_b formed on the fly from the read-only CG vectors),
+// stores s_a (sc1, drained) and takes a ticket; the last block to arrive
+// finalises every column (col_finalize: the CG vectors are written only
+// once nobody reads them) and publishes the CG scalars itself.  FIN false
+// (many features): s into acc only, k_fin finalises.
+// QB blocks per feature split its adjacency (about one entry per subgroup:
+// one round of loads), each storing its partial slot acc[a QB + q]; the last
+// block sums a feature's QB slots in slot order.
+template <typename real, int KP, bool FIN>
+__global__ __launch_bounds__(BLOCK) void k_pg_step(uint64_t D, uint32_t QB, const int64_t *__restrict__ aptr,
+                                                   const uint32_t *__restrict__ apair,
+                                                   const uint32_t *__restrict__ aoth, const real *__restrict__ G,
+                                                   real *__restrict__ part, Fin<real> f) {
+  using Gm = Geo<real, KP>;
+  if (!f.st->run[f.it]) return;
+  const bool upd = f.it > 1;
+  const real alpha = upd ? (real)f.st->alpha : (real)0, beta = upd ? (real)f.st->beta : (real)0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int sg = lane / Gm::LPR, li = lane % Gm::LPR;
+  const int sid = w * Gm::NSG + sg;
+  __shared__ __align__(16) real red[BLOCK / 64][KP];
+  for (uint64_t bq = blockIdx.x; bq < D * QB; bq += gridDim.x) {
+    const uint64_t a = bq / QB;
+    const int64_t t0 = aptr[a], t1 = aptr[a + 1];
+    vec_t<real> s = vzero<real>();
+    for (int64_t t = t0 + (int64_t)(bq % QB) * 4 * Gm::NSG + sid; t < t1; t += (int64_t)QB * 4 * Gm::NSG) {
+      const uint32_t p = apair[t], b = aoth[t];
+      const vec_t<real> vb = cg_dir_at<real, KP>(f.P, f.R, f.Hp, alpha, beta, upd, (size_t)b * KP + li * Gm::VE);
+      const real *Gp = G + (size_t)p * KP * KP;  // symmetric: G v = v G
+      if constexpr (KP >= 64) s += sg_vecmat_rolled<real, KP, 4>(vb, Gp, li);
+      else s += sg_vecmat<real, KP>(vb, Gp, li);
+    }
+    s = xsg_vsum<Gm::LPR, real>(s);
+    if (sg == 0) *reinterpret_cast<vec_t<real> *>(&red[w][li * Gm::VE]) = s;
+    __syncthreads();
+    if (w == 0 && sg == 0) {  // the waves' sums in wave order
+      vec_t<real> t = *reinterpret_cast<const vec_t<real> *>(&red[0][li * Gm::VE]);
+#pragma unroll
+      for (int q = 1; q < BLOCK / 64; q++) t += *reinterpret_cast<const vec_t<real> *>(&red[q][li * Gm::VE]);
+#pragma unroll
+      for (int e = 0; e < Gm::VE; e++)
+        __hip_atomic_store(part + bq * KP + li * Gm::VE + e, t[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+  }
+  if (w == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's partial slots landed
+  __syncthreads();
+  const double z[1] = {0.0};
+  double tz[1];
+  if (!last_block<1>(z, f.part, f.tick, tz)) return;
+  // the last block: each feature's slots in order, then (FIN) the
+  // finalisation of every column and the CG scalars, else s into acc
+  const BufView pb = buf_view(part, D * QB * KP * sizeof(real));
+  double dsum[3] = {0, 0, 0};
+  for (uint64_t q = threadIdx.x; q < D * Gm::LPR; q += BLOCK) {
+    const uint32_t c = (uint32_t)(q / Gm::LPR);
+    const int l = (int)(q % Gm::LPR);
+    FinOps<real> ops;
+    if constexpr (FIN) ops = fin_load<real, KP, 1>(f, c, upd, l);
+    vec_t<real> sv = vzero<real>();
+    for (uint32_t u = 0; u < QB; u++)
+      sv += bld_sc1<real>(pb, (uint32_t)((((size_t)c * QB + u) * KP + l * Gm::VE) * sizeof(real)));
+    if constexpr (FIN) col_finalize<real, KP, 1>(f, c, sv, alpha, beta, upd, l, dsum, ops);
+    else vst<real>(f.acc + (size_t)c * KP + l * Gm::VE, sv);
+  }
+  if constexpr (FIN) {
+    double tot[3] = {block_sum(dsum[0]), block_sum(dsum[1]), block_sum(dsum[2])};
+    if (threadIdx.x == 0) {
+      if (f.dots) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) f.dots[k] = tot[k];
+      } else {
+        cg_publish<real, 1>(f, tot);
+      }
+    }
+  }
+}
+
 // ------------------------------------------ persistent column-Gram CG ---
 // Every CG step of a half whose Hessian-vector product is the D column
 // Grams (k_hv_cgram: the genre / artist side halves, the column-Gram cross
@@ -2296,6 +2400,75 @@ __global__ __launch_bounds__(BLOCK) void k_feat(uint64_t nwave, const Job *__res
   // (last_block); waves that stored none do not wait for their vector stores
   // (wave jobs are wave-uniform, so is the flag)
   if (__any(hd_stored)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (MODE != 2) fin_blocks<real, (MODE == 2 ? 0 : MODE)>(f, dsum);
+}
+
+// Feature pass of a field whose columns are few and heavy (round 5; the
+// kkbox context field: 120 columns of ~500 rows, ~1,300 segments): ONE
+// BLOCK PER COLUMN.  Its 4 NSG subgroups take FE consecutive entries each
+// per round (all their row loads in flight), the column's sum is reduced
+// through LDS in a fixed order and finalised by one subgroup, whose
+// finalisation operands were loaded at the start; the grid's dot products
+// by the last block (fin_blocks).  k_feat instead cuts such a column into
+// wave-chunks whose partial slots the last-arriving chunk sums: a chain of
+// dependent rounds (~15 us per context step).  Deterministic (fixed grid).
+// MODE as k_feat (no column tau).
+template <typename real, int KP, int MODE>
+__global__ __launch_bounds__(BLOCK) void k_feat_col(uint64_t D, const int64_t *__restrict__ cptr,
+                                                    const uint32_t *__restrict__ crow, const real *__restrict__ cval,
+                                                    const real *__restrict__ h, uint64_t hbytes, Fin<real> f) {
+  using Gm = Geo<real, KP>;
+  constexpr int FE = 8;  // entries per subgroup and round
+  constexpr int U = (FE + Gm::LPR - 1) / Gm::LPR;
+  if (f.it > 0 && !f.st->run[f.it]) return;
+  const BufView hb = buf_view(h, hbytes);
+  const bool upd = MODE == 1 && f.it > 1;
+  const real alpha = upd ? (real)f.st->alpha : (real)0, beta = upd ? (real)f.st->beta : (real)0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int sg = lane / Gm::LPR, li = lane % Gm::LPR;
+  const int sid = w * Gm::NSG + sg;
+  constexpr int NS = 4 * Gm::NSG;
+  __shared__ __align__(16) real red[BLOCK / 64][KP];
+  double dsum[3] = {0, 0, 0};
+  for (uint64_t c = blockIdx.x; c < D; c += gridDim.x) {
+    const bool fin = w == 0 && sg == 0;
+    FinOps<real> ops;
+    if (MODE != 2 && fin) ops = fin_load<real, KP, (MODE == 2 ? 0 : MODE)>(f, (uint32_t)c, upd, li);
+    const int64_t b = cptr[c], e = cptr[c + 1];
+    vec_t<real> s = vzero<real>();
+    for (int64_t t0 = b + (int64_t)sid * FE; t0 < e; t0 += (int64_t)NS * FE) {
+      uint32_t rr[U];
+      real vv[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int64_t t = t0 + li + u * Gm::LPR;
+        const bool ok = li + u * Gm::LPR < FE && t < e;
+        rr[u] = ok ? crow[t] : 0u;
+        vv[u] = ok ? cval[t] : (real)0;
+      }
+      vec_t<real> hv[FE];
+      sfor<FE>([&](auto E) {
+        constexpr int q = decltype(E)::value;
+        const uint32_t r = sg_bcast<Gm::LPR, q % Gm::LPR>(rr[q / Gm::LPR], li);
+        const real x = sg_bcast<Gm::LPR, q % Gm::LPR>(vv[q / Gm::LPR], li);
+        const uint32_t off = t0 + q < e ? r * (uint32_t)(KP * sizeof(real)) + li * LANE_B<real> : hb.oob;
+        hv[q] = vsplat<real>(x) * bld<real>(hb, off);
+      });
+#pragma unroll
+      for (int q = 0; q < FE; q++) s += hv[q];
+    }
+    s = xsg_vsum<Gm::LPR, real>(s);
+    if (sg == 0) *reinterpret_cast<vec_t<real> *>(&red[w][li * Gm::VE]) = s;
+    __syncthreads();
+    if (fin) {  // the waves' sums in wave order
+      vec_t<real> t = *reinterpret_cast<const vec_t<real> *>(&red[0][li * Gm::VE]);
+#pragma unroll
+      for (int q = 1; q < BLOCK / 64; q++) t += *reinterpret_cast<const vec_t<real> *>(&red[q][li * Gm::VE]);
+      if constexpr (MODE == 2) vst<real>(f.acc + c * KP + li * Gm::VE, t);
+      else col_finalize<real, KP, (MODE == 2 ? 0 : MODE)>(f, (uint32_t)c, t, alpha, beta, upd, li, dsum, ops);
+    }
+    __syncthreads();
+  }
   if (MODE != 2) fin_blocks<real, (MODE == 2 ? 0 : MODE)>(f, dsum);
 }
 

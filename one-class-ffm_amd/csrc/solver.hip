@@ -155,6 +155,24 @@ template <typename real> struct DevField {
   DevBuf<uint32_t> segd;  // one: the node of each positive segment's row (no row indirection)
   DevBuf<real> segx;
   std::unique_ptr<ItemOwned<real>> io;  // item-owned CG steps (item-id field, several ranks)
+  // Pair Grams (kernels.hpp k_pg_step; several nodes per row, few
+  // features): pairs p = (pa, pb), pa <= pb, of features met in one row;
+  // their entries (row, X_ia X_ib) pair-major with Gram build chunks; each
+  // feature's adjacency (its pairs and the other feature of each).
+  bool pg = false;
+  uint64_t npair = 0;
+  DevBuf<uint32_t> ppa, ppb, pgrow;
+  DevBuf<real> pgval, pgram, pgpart;
+  DevBuf<Job> pgchunks, pgsums;
+  uint64_t pgslots = 0;
+  DevBuf<unsigned> pgcnt;
+  DevBuf<int64_t> paptr;  // per feature a: its pairs (pair, other feature) in papair / paoth
+  DevBuf<uint32_t> papair, paoth;
+  uint32_t pqb = 1;  // k_pg_step blocks per feature
+  // column pointers of the row / segment CSC for the column-block feature
+  // pass (k_feat_col; derived from the jobs on first use)
+  DevBuf<int64_t> fcptr[2];
+  int fcol[2] = {-1, -1};  // -1 not decided, 0 no, 1 yes
   // host copies kept until the segment CSC is built
   std::vector<int64_t> h_xptr;
   std::vector<uint32_t> h_xidx;
@@ -474,6 +492,12 @@ template <typename real> class Problem final : public ProblemBase {
       for (uint32_t fi = 0; fi < sd->F.size(); fi++)
         if (ccg_field_all(*sd->F[fi], *sd, sd == &U_, fi, U)) ccg_setup(*sd->F[fi], *sd);
     if (io_mode_ != 0 && comm_.active() && (comm_.nranks > 1 || io_mode_ == 2) && C_ > 0) io_setup(U, V);
+    // pair Grams of the side halves of low-cardinality multi-node fields
+    // (one GPU: every rank would otherwise have to agree on its local shard's
+    // pair count, and the multi-rank path has its own partial-sum protocol)
+    if (pgram_mode_ != 0 && !comm_.active() && prm_.self_side)
+      for (DevSide<real> *sd : {&U_, &V_})
+        for (uint32_t fi = 0; fi < sd->F.size(); fi++) pgram_setup(*sd->F[fi], *sd);
     // T pre-pass rows: the larger side that takes the pre-pass (tpre() also
     // bounds R for 32-bit buffer offsets, so test each side on its own)
     uint64_t tR = 0;
@@ -1937,6 +1961,21 @@ template <typename real> class Problem final : public ProblemBase {
           else go2(ml, std::integral_constant<int, BM_IN>());
         };
         if (tp) bytes += (double)own.R * KP * rs - (double)C_ * own.R * KP * rs;  // one T row instead of C table rows
+        if constexpr (OCFFM_GD_PROBE) {  // the gathers alone (kernels.hpp PRB), timed as their own family
+          auto probe = [&](auto bm) {
+            constexpr int BM = decltype(bm)::value;
+            launch(k_gd_cross_seg<real, KP, false, BM, false, true>, grid_for(own.nseg, 4 * Gm::NSG, gd_blocks_), BLOCK,
+                   0, own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
+                   (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, h.partner->bias.p, w_,
+                   r_, h_.p, (uint64_t)h.partner->R, cur, drow, dxs, (const uint32_t *)own.perm.p,
+                   (const real *)nullptr, via ? (const real *)h.partner->yt.p : (const real *)nullptr);
+          };
+          prof_launch("gd_probe", bytes, [&] {
+            if (!cur) probe(std::integral_constant<int, BM_FULL>());
+            else if (enter) probe(std::integral_constant<int, BM_ENTER>());
+            else probe(std::integral_constant<int, BM_IN>());
+          });
+        }
         prof_launch("gd_cross_row", bytes, [&] {
           if (lds && !tp) go(std::true_type());
           else go(std::false_type());
@@ -2360,7 +2399,187 @@ template <typename real> class Problem final : public ProblemBase {
     return build + c * gstep <= c * rstep;
   }
 
+  // ---- pair Grams (kernels.hpp k_pg_step; OCFFM_PGRAM: 0 off, 1 where
+  // the gate below passes, 2 wherever the structure allows)
+  int pgram_mode_ = std::getenv("OCFFM_PGRAM") ? std::atoi(std::getenv("OCFFM_PGRAM")) : 1;
+  static constexpr uint64_t PG_FIN1 = 1024;  // k_pg_step finalises in its last block up to this many features
+  DevBuf<real> pgt_;                          // its per-(feature, block) partial slots
+  bool pgram(const HalfCtx &h) const { return !h.cross && h.F->pg; }
+  // The field's pairs, entries and CSCs from its rows (host; once).  Gate:
+  // several nodes per row (one node: the per-column Grams), not owned, at
+  // most PG_FIN1 features (the single-launch step), and (mode 1) a CG step reading the pair Grams
+  // (npair k^2) costs at most what the row pass reads for the partner rows
+  // times 8 (npair k <= 8 R): the kkbox context field has ~7,200 pairs over
+  // 30,755 rows (0.93 of the bound).
+  void pgram_setup(DevField<real> &F, DevSide<real> &sd) {
+    const uint64_t R = sd.R;
+    if (F.one || F.idlike || F.excl || R == 0 || F.nnz == 0 || F.D == 0) return;
+    if (pgram_mode_ == 1 && F.D > PG_FIN1) return;
+    std::vector<int64_t> xp(R + 1);
+    std::vector<uint32_t> xi(F.nnz);
+    std::vector<real> xv(F.nnz);
+    HIPCHK(hipMemcpy(xp.data(), F.xptr.p, xp.size() * sizeof(int64_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(xi.data(), F.xidx.p, xi.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(xv.data(), F.xval.p, xv.size() * sizeof(real), hipMemcpyDeviceToHost));
+    struct Ent {
+      uint64_t key;
+      uint32_t row;
+      double w;
+    };
+    std::vector<Ent> ent;
+    std::vector<std::pair<uint32_t, double>> nd;
+    for (uint64_t i = 0; i < R; i++) {
+      nd.clear();  // the row's vector X_i: nodes by feature, repeats summed
+      for (int64_t q = xp[i]; q < xp[i + 1]; q++) nd.push_back({xi[q], (double)xv[q]});
+      std::sort(nd.begin(), nd.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
+      size_t u = 0;
+      for (size_t q = 0; q < nd.size(); q++) {
+        if (u && nd[u - 1].first == nd[q].first) nd[u - 1].second += nd[q].second;
+        else nd[u++] = nd[q];
+      }
+      nd.resize(u);
+      for (size_t x = 0; x < u; x++)
+        for (size_t y = x; y < u; y++)
+          ent.push_back(Ent{(uint64_t)nd[x].first * F.D + nd[y].first, (uint32_t)i, nd[x].second * nd[y].second});
+    }
+    std::stable_sort(ent.begin(), ent.end(), [](const Ent &x, const Ent &y) { return x.key < y.key; });
+    std::vector<uint32_t> pa, pb, prow;
+    std::vector<double> pw;
+    std::vector<int64_t> pptr{0};
+    for (uint64_t q = 0; q < ent.size(); q++) {
+      if (q == 0 || ent[q].key != ent[q - 1].key) {
+        if (q) pptr.push_back((int64_t)q);
+        pa.push_back((uint32_t)(ent[q].key / F.D));
+        pb.push_back((uint32_t)(ent[q].key % F.D));
+      }
+      prow.push_back(ent[q].row);
+      pw.push_back(ent[q].w);
+    }
+    pptr.push_back((int64_t)ent.size());
+    const uint64_t np = pa.size();
+    const double gb = (double)np * kp_ * kp_ * sizeof(real);
+    if (np == 0 || np > (1ull << 24) || gb > 1.0 * (1ull << 30)) return;
+    if (pgram_mode_ == 1 && (double)np * kp_ > 8.0 * (double)R) return;
+    F.npair = np;
+    F.ppa.upload(pa);
+    F.ppb.upload(pb);
+    F.pgrow.upload(prow);
+    F.pgval.upload(to_real(pw));
+    // Gram build chunks (col_gram_chunks' cut, over the pairs' entries)
+    const uint64_t ch = cgram32() ? (uint64_t)CGRAM32_ROWS
+                                  : std::min<uint64_t>(cgram_chunk_, (uint64_t)cgram_rows((int)kp_, (int)sizeof(real)));
+    std::vector<Job> chunks, sums;
+    uint64_t slots = 0;
+    for (uint64_t d = 0; d < np; d++) {
+      const uint64_t b = pptr[d], e = pptr[d + 1];
+      const uint32_t n = (uint32_t)std::max<uint64_t>(1, (e - b + ch - 1) / ch);
+      for (uint32_t q = 0; q < n; q++)
+        chunks.push_back(Job{(uint32_t)d, n, n > 1 ? (uint32_t)(slots + q) : 0u, q, (int64_t)std::min(e, b + q * ch),
+                             (int64_t)std::min(e, b + (q + 1) * ch)});
+      if (n > 1) sums.push_back(Job{(uint32_t)d, n, (uint32_t)slots, 0u, 0, 0});
+      if (n > 1) slots += n;
+    }
+    F.pgchunks.upload(chunks);
+    if (cgram32() && !sums.empty()) F.pgsums.upload(sums);
+    F.pgslots = slots;
+    F.pgcnt.alloc(np);
+    // adjacency: feature a <- (p, b) for p = (a, b), and b <- (p, a) for a != b
+    std::vector<int64_t> ap(F.D + 1, 0);
+    for (uint64_t d = 0; d < np; d++) {
+      ap[pa[d] + 1]++;
+      if (pa[d] != pb[d]) ap[pb[d] + 1]++;
+    }
+    for (uint64_t d = 0; d < F.D; d++) ap[d + 1] += ap[d];
+    std::vector<uint32_t> apair((size_t)ap[F.D]), aoth((size_t)ap[F.D]);
+    std::vector<int64_t> cur(ap.begin(), ap.end() - 1);
+    for (uint64_t d = 0; d < np; d++) {
+      apair[(size_t)cur[pa[d]]] = (uint32_t)d;
+      aoth[(size_t)cur[pa[d]]++] = pb[d];
+      if (pa[d] != pb[d]) {
+        apair[(size_t)cur[pb[d]]] = (uint32_t)d;
+        aoth[(size_t)cur[pb[d]]++] = pa[d];
+      }
+    }
+    F.paptr.upload(ap);
+    F.papair.upload(apair);
+    F.paoth.upload(aoth);
+    // blocks per feature: about one adjacency entry per subgroup
+    uint64_t amax = 1;
+    for (uint64_t d = 0; d < F.D; d++) amax = std::max<uint64_t>(amax, (uint64_t)(ap[d + 1] - ap[d]));
+    const uint64_t per = 4 * (uint64_t)nsg();
+    F.pqb = (uint32_t)std::min<uint64_t>(8, (amax + per - 1) / per);
+    if (F.D * F.pqb * kp_ > pgt_.n) pgt_.alloc(F.D * F.pqb * kp_);
+    F.pg = true;
+  }
+  // The half's pair Grams (k_col_gram* with pair weights: d_i X_ia X_ib).
+  void pair_grams(const HalfCtx &h) {
+    DevField<real> &F = *h.F;
+    if (!F.pgram.p) F.pgram.alloc(F.npair * kp_ * kp_, false);
+    if (F.pgslots && !F.pgpart.p) F.pgpart.alloc(F.pgslots * kp_ * kp_, false);
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      const double rs = sizeof(real);
+      prof_launch("pair_gram", (double)F.pgrow.n * (8 + rs + 16 + KP * rs) + (double)F.pgram.bytes(), [&] {
+        if constexpr (std::is_same<real, float>::value && KP == 32) {
+          if (cgram32()) {
+            launch(k_col_gram32, (unsigned)((F.pgchunks.n + 3) / 4), BLOCK, 0, (uint64_t)F.pgchunks.n,
+                   (const Job *)F.pgchunks.p, (const uint32_t *)F.pgrow.p, (const float *)F.pgval.p, hess_cnt(h),
+                   (const float *)h.Q1, (uint64_t)h.own->R, w_, hess_n1(h), (float *)F.pgram.p, (float *)F.pgpart.p,
+                   1);
+            if (F.pgsums.n)
+              launch(k_gram_slot_sum, (unsigned)F.pgsums.n, BLOCK, 0, (const Job *)F.pgsums.p,
+                     (const float *)F.pgpart.p, (float *)F.pgram.p);
+            return;
+          }
+        }
+        if constexpr (std::is_same<real, double>::value && KP == 32) {
+          if (cgram32()) {
+            launch(k_col_gram_f64, (unsigned)((F.pgchunks.n + 3) / 4), BLOCK, 0, (uint64_t)F.pgchunks.n,
+                   (const Job *)F.pgchunks.p, (const uint32_t *)F.pgrow.p, (const double *)F.pgval.p, hess_cnt(h),
+                   (const double *)h.Q1, (uint64_t)h.own->R, w_, hess_n1(h), (double *)F.pgram.p,
+                   (double *)F.pgpart.p, 1);
+            if (F.pgsums.n)
+              launch(k_hot_slot_sum<double, 32>, dim3((unsigned)F.pgsums.n, (1024 + BLOCK - 1) / BLOCK), BLOCK, 0,
+                     (const Job *)F.pgsums.p, (const double *)F.pgpart.p, (double *)F.pgram.p);
+            return;
+          }
+        }
+        launch(k_col_gram<real, KP>, (unsigned)F.pgchunks.n, BLOCK, 0, F.pgchunks.p, F.pgrow.p, F.pgval.p,
+               hess_cnt(h), h.Q1, w_, hess_n1(h), F.pgram.p, F.pgpart.p, F.pgcnt.p, 1);
+      });
+    });
+  }
+  // One CG step of a pair-Gram half: one launch (k_pg_step), or with many
+  // features the pair products into acc and the unfused finalisation.
+  void pair_pass(HalfCtx &h, int it) {
+    DevField<real> &F = *h.F;
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      using Gm = Geo<real, KP>;
+      const double rs = sizeof(real);
+      const Fin<real> fin = make_fin(h, it);
+      const uint32_t QB = F.pqb;
+      const unsigned grid = (unsigned)std::min<uint64_t>(F.D * QB, 8192);
+      const double bytes = (double)F.paoth.n * (KP * KP * rs + 8) + (double)F.D * KP * rs * (it > 1 ? 9 : 4);
+      prof_launch("pg_step", bytes, [&] {
+        if (F.D <= PG_FIN1) {
+          launch(k_pg_step<real, KP, true>, grid, BLOCK, 0, (uint64_t)F.D, QB, (const int64_t *)F.paptr.p,
+                 (const uint32_t *)F.papair.p, (const uint32_t *)F.paoth.p, (const real *)F.pgram.p, pgt_.p, fin);
+          return;
+        }
+        launch(k_pg_step<real, KP, false>, grid, BLOCK, 0, (uint64_t)F.D, QB, (const int64_t *)F.paptr.p,
+               (const uint32_t *)F.papair.p, (const uint32_t *)F.paoth.p, (const real *)F.pgram.p, pgt_.p, fin);
+        const uint64_t nv = h.D * KP / Gm::VE;
+        launch(k_fin<real, KP, 1>, grid_for(nv, BLOCK, 2048), BLOCK, 0, nv, fin);
+      });
+    });
+  }
+
   void col_grams(const HalfCtx &h) {
+    if (pgram(h)) {
+      pair_grams(h);
+      return;
+    }
     if (!cgram(h)) return;
     if (h.cross) {
       ccg_build(h);
@@ -2379,7 +2598,7 @@ template <typename real> class Problem final : public ProblemBase {
             // (q1: the same-side partner table, one row per row of this side)
             launch(k_col_gram32, (unsigned)((F.gchunks.n + 3) / 4), BLOCK, 0, (uint64_t)F.gchunks.n,
                    (const Job *)F.gchunks.p, (const uint32_t *)F.crow.p, (const float *)F.cval.p, hess_cnt(h),
-                   (const float *)h.Q1, (uint64_t)h.own->R, w_, hess_n1(h), (float *)F.gram.p, (float *)F.gpart.p);
+                   (const float *)h.Q1, (uint64_t)h.own->R, w_, hess_n1(h), (float *)F.gram.p, (float *)F.gpart.p, 0);
             if (F.gsums.n)
               launch(k_gram_slot_sum, (unsigned)F.gsums.n, BLOCK, 0, (const Job *)F.gsums.p,
                      (const float *)F.gpart.p, (float *)F.gram.p);
@@ -2391,7 +2610,7 @@ template <typename real> class Problem final : public ProblemBase {
             launch(k_col_gram_f64, (unsigned)((F.gchunks.n + 3) / 4), BLOCK, 0, (uint64_t)F.gchunks.n,
                    (const Job *)F.gchunks.p, (const uint32_t *)F.crow.p, (const double *)F.cval.p, hess_cnt(h),
                    (const double *)h.Q1, (uint64_t)h.own->R, w_, hess_n1(h), (double *)F.gram.p,
-                   (double *)F.gpart.p);
+                   (double *)F.gpart.p, 0);
             if (F.gsums.n)
               launch(k_hot_slot_sum<double, 32>, dim3((unsigned)F.gsums.n, (1024 + BLOCK - 1) / BLOCK), BLOCK, 0,
                      (const Job *)F.gsums.p, (const double *)F.gpart.p, (double *)F.gram.p);
@@ -2399,7 +2618,7 @@ template <typename real> class Problem final : public ProblemBase {
           }
         }
         launch(k_col_gram<real, KP>, (unsigned)F.gchunks.n, BLOCK, 0, F.gchunks.p, F.crow.p, F.cval.p,
-               hess_cnt(h), h.Q1, w_, hess_n1(h), F.gram.p, F.gpart.p, F.cnt.p);
+               hess_cnt(h), h.Q1, w_, hess_n1(h), F.gram.p, F.gpart.p, F.cnt.p, 0);
       });
     });
   }
@@ -2446,10 +2665,77 @@ template <typename real> class Problem final : public ProblemBase {
   // One feature pass (kernels.hpp: k_feat) over the row or segment CSC of
   // the half's field.  mode 0/1 finalise (gradient / Hessian-vector of CG
   // iteration it); mode 2 stores the column sums into acc_.
+  // Column-block feature pass (kernels.hpp k_feat_col): a field with few,
+  // heavy columns (at most 4,096 columns of 64 entries or more on average),
+  // not owned (its CSC's unowned columns have no jobs), no column tau.
+  int feat_col_mode_ = std::getenv("OCFFM_FEATCOL") ? std::atoi(std::getenv("OCFFM_FEATCOL")) : 1;
+  bool feat_col(HalfCtx &h, bool seg, int mode) {
+    DevField<real> &F = *h.F;
+    const int ix = seg ? 1 : 0;
+    if (feat_col_mode_ == 0 || F.excl || (mode != 0 && coltau(h))) return false;
+    if (F.fcol[ix] < 0) {
+      F.fcol[ix] = 0;
+      const uint64_t ent = seg ? F.scrow.n : F.crow.n;
+      const uint64_t nj = (seg ? F.snjw : F.njw) * (uint64_t)nsg();
+      if (F.D > 0 && F.D <= 4096 && nj && (feat_col_mode_ == 2 || ent >= 64 * F.D)) {
+        std::vector<Job> jobs(nj);
+        HIPCHK(hipMemcpy(jobs.data(), seg ? F.sjobs.p : F.jobs.p, nj * sizeof(Job), hipMemcpyDeviceToHost));
+        std::vector<int64_t> first(F.D, INT64_MAX), last(F.D, -1), cp(F.D + 1, 0);
+        for (const Job &j : jobs)
+          if (j.col != JOB_NONE && j.col < F.D) {
+            first[j.col] = std::min(first[j.col], j.b);
+            last[j.col] = std::max(last[j.col], j.e);
+          }
+        bool ok = true;
+        for (uint64_t c = 0; c < F.D && ok; c++) {
+          if (last[c] < 0) {
+            cp[c + 1] = cp[c];
+          } else {
+            ok = first[c] == cp[c];
+            cp[c + 1] = last[c];
+          }
+        }
+        if (ok && (uint64_t)cp[F.D] == ent) {
+          F.fcptr[ix].upload(cp);
+          F.fcol[ix] = 1;
+        }
+      }
+    }
+    return F.fcol[ix] == 1;
+  }
+
   void feat_launch(HalfCtx &h, int it, bool seg, int mode) {
     DevField<real> &F = *h.F;
     const uint64_t njw = seg ? F.snjw : F.njw;
     if (!njw) return;
+    if (feat_col(h, seg, mode)) {
+      with_kp(kp_, [&](auto K) {
+        constexpr int KP = decltype(K)::value;
+        const double rs = sizeof(real);
+        const uint64_t ent = seg ? F.scrow.n : F.crow.n;
+        const double vecs = mode == 2 ? 1 : (mode == 0 ? 5 : (it > 1 ? 8 : 3));
+        const double bytes = (double)ent * (4 + rs) + (double)ent * KP * rs + (double)F.D * 8 +
+                             (double)h.D * KP * rs * vecs;
+        const char *name = mode == 2 ? "csc_scatter" : (mode == 0 ? "feat_grad" : "feat_hv");
+        Fin<real> fin = make_fin(h, it);
+        const uint32_t *crow = seg ? F.scrow.p : F.crow.p;
+        const real *cval = seg ? F.scval.p : F.cval.p;
+        const int64_t *cp = F.fcptr[seg ? 1 : 0].p;
+        const unsigned grid = (unsigned)std::min<uint64_t>(F.D, 4096);
+        prof_launch(name, bytes, [&] {
+          if (mode == 0)
+            launch(k_feat_col<real, KP, 0>, grid, BLOCK, 0, (uint64_t)F.D, cp, crow, cval, (const real *)h_.p,
+                   (uint64_t)h_.bytes(), fin);
+          else if (mode == 1)
+            launch(k_feat_col<real, KP, 1>, grid, BLOCK, 0, (uint64_t)F.D, cp, crow, cval, (const real *)h_.p,
+                   (uint64_t)h_.bytes(), fin);
+          else
+            launch(k_feat_col<real, KP, 2>, grid, BLOCK, 0, (uint64_t)F.D, cp, crow, cval, (const real *)h_.p,
+                   (uint64_t)h_.bytes(), fin);
+        });
+      });
+      return;
+    }
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
       using Gm = Geo<real, KP>;
@@ -2465,31 +2751,33 @@ template <typename real> class Problem final : public ProblemBase {
       const Job *jobs = seg ? F.sjobs.p : F.jobs.p;
       const uint32_t *crow = seg ? F.scrow.p : F.crow.p;
       const real *cval = seg ? F.scval.p : F.cval.p;
+      real *hb = h_.p;
+      const uint64_t hbytes = h_.bytes();
       const char *name = mode == 2 ? "csc_scatter" : (mode == 0 ? "feat_grad" : "feat_hv");
       const real *nq = nullptr;
       prof_launch(name, bytes, [&] {
         if (mode == 0) {
-          launch(k_feat<real, KP, 0>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, wpart_.bytes(), fin, nq);
+          launch(k_feat<real, KP, 0>, grid, BLOCK, 0, njw, jobs, crow, cval, hb, hbytes, wpart_.p, wpart_.bytes(), fin, nq);
         } else if (mode == 1) {
           if constexpr ((size_t)KP * KP * sizeof(real) <= COLTAU_LDS) {
             if (coltau(h)) {
               fin.xsq = F.xsq.p;
               launch(k_feat<real, KP, 1, JOB_ENT, true>, grid, BLOCK, (size_t)KP * KP * sizeof(real), njw, jobs, crow,
-                     cval, h_.p, h_.bytes(), wpart_.p, wpart_.bytes(), fin, (const real *)qtq_);
+                     cval, hb, hbytes, wpart_.p, wpart_.bytes(), fin, (const real *)qtq_);
               return;
             }
           }
-          launch(k_feat<real, KP, 1>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, wpart_.bytes(), fin, nq);
+          launch(k_feat<real, KP, 1>, grid, BLOCK, 0, njw, jobs, crow, cval, hb, hbytes, wpart_.p, wpart_.bytes(), fin, nq);
         } else {
           if constexpr ((size_t)KP * KP * sizeof(real) <= COLTAU_LDS) {
             if (coltau(h) && it > 0) {
               fin.xsq = F.xsq.p;
               launch(k_feat<real, KP, 2, JOB_ENT, true>, grid, BLOCK, (size_t)KP * KP * sizeof(real), njw, jobs, crow,
-                     cval, h_.p, h_.bytes(), wpart_.p, wpart_.bytes(), fin, (const real *)qtq_);
+                     cval, hb, hbytes, wpart_.p, wpart_.bytes(), fin, (const real *)qtq_);
               return;
             }
           }
-          launch(k_feat<real, KP, 2>, grid, BLOCK, 0, njw, jobs, crow, cval, h_.p, h_.bytes(), wpart_.p, wpart_.bytes(), fin, nq);
+          launch(k_feat<real, KP, 2>, grid, BLOCK, 0, njw, jobs, crow, cval, hb, hbytes, wpart_.p, wpart_.bytes(), fin, nq);
         }
       });
     });
@@ -2746,8 +3034,14 @@ template <typename real> class Problem final : public ProblemBase {
 
   // Persistent column-Gram CG (k_cg_cgram): one GPU (or a replicated half:
   // no collective inside), the plain expanded residual, not item-owned.
+  // Only where the step kernel's own grid fits one block per CU (genre,
+  // artist): a persistent grid is capped there, and on config 5's 250 k
+  // columns that cap cost the Gram stream its occupancy (5.0 -> 5.3 s per
+  // epoch with the persistent kernel on every column-Gram half).
   bool cgp_ok(const HalfCtx &h) const {
-    return cgp_on_ && cgram(h) && (!comm_.active() || repl(h)) && !exact_r2(h) && !io_half(h) && h.D > 0;
+    const uint64_t per_block = 4 * (uint64_t)nsg();
+    return cgp_on_ && cgram(h) && (!comm_.active() || repl(h)) && !exact_r2(h) && !io_half(h) && h.D > 0 &&
+           (h.D + per_block - 1) / per_block <= ncu_;
   }
   double cgp_step_bytes(const HalfCtx &h) const {
     return (double)h.D * kp_ * kp_ * sizeof(real) + (double)h.D * kp_ * sizeof(real) * 9;
@@ -2806,6 +3100,10 @@ template <typename real> class Problem final : public ProblemBase {
         prof_launch("hv_fin", (double)h.D * KP * rs * (it > 1 ? 9 : 4),
                     [&] { launch(k_fin<real, KP, 1>, grid_for(nv, BLOCK, 2048), BLOCK, 0, nv, fin); });
       });
+      return;
+    }
+    if (pgram(h)) {
+      pair_pass(h, it);
       return;
     }
     const bool fz_ = fused_rows(h);

@@ -257,8 +257,8 @@ def test_epochs_fp32_tiny(tiny, k):
 
 
 @pytest.mark.parametrize("variant", ["ns", "freq", "k5", "k16", "multi_nnz", "k1", "k64", "k100", "k128", "sparse",
-                                     "kdd12", "outbrain", "wide_ns"])
-def test_variants_fp64(variant):
+                                     "kdd12", "outbrain", "wide_ns", "multi_nnz_pg", "freq_pg", "k64_pg"])
+def test_variants_fp64(variant, monkeypatch):
     """Flags and shapes: --ns, --freq, k = 1 / 5 / 16 / 64 / 100 / 128 (padded
     rows of 4 .. 128: one to 64 lanes per row; 128 is the largest k the
     library takes), several nodes per field, a sparse
@@ -267,6 +267,14 @@ def test_variants_fp64(variant):
     kdd12-shape (fu=2, fv=4, k=16), outbrain-shape (fu=2, fv=2, k=64, ~1
     positive per row) and the wide --ns set (fu=39, fv=1: 39 cross blocks)."""
     kw = {}
+    if variant.endswith("_pg"):
+        # pair Grams (k_hs_pair) forced on every multi-node field's side
+        # halves: real-valued nodes, repeated features in a row, --freq, k = 64
+        monkeypatch.setenv("OCFFM_PGRAM", "2")
+        variant = variant[:-3]
+        if variant != "multi_nnz":
+            ds0 = synth.general(seed=19, m=300, n=80, fu=2, fv=2, k=8, nnz_user=3, mean_pos=4.0, vals="real",
+                                test_rows=30)
     if variant == "kdd12":
         ds = synth.general(seed=31, m=400, n=120, fu=2, fv=4, k=16, mean_pos=3.0, test_rows=40, name="kdd12")
     elif variant == "outbrain":
@@ -282,6 +290,8 @@ def test_variants_fp64(variant):
                            test_rows=20)
     else:
         ds = synth.tiny(seed=4, m=300 if variant in ("k64", "k100", "k128") else 1000)
+    if os.environ.get("OCFFM_PGRAM") == "2" and variant != "multi_nnz":
+        ds = ds0
     for name, k in (("k1", 1), ("k5", 5), ("k16", 16), ("k64", 64), ("k100", 100), ("k128", 128)):
         if variant == name:
             kw["k"] = k
@@ -416,7 +426,8 @@ def test_heavy_columns(precision, cgram, monkeypatch):
         assert abs(gpu_objective(o2, g) - f_ref) <= 1e-3 * abs(f_ref)
 
 
-@pytest.mark.parametrize("ds_name", ["heavy", "kkbox_s", "kkbox_s_cgram2", "cfg5", "cfg5_k32", "cfg5_nomfma"])
+@pytest.mark.parametrize("ds_name", ["heavy", "kkbox_s", "kkbox_s_cgram2", "kkbox_s_pgram2", "cfg5", "cfg5_k32",
+                                     "cfg5_nomfma"])
 def test_fp32_runs_bit_identical(ds_name, monkeypatch):
     """The default fp32 path has no order-dependent float sums (feature
     passes, Gram builds and grid reductions combine in a fixed order): two
@@ -434,6 +445,8 @@ def test_fp32_runs_bit_identical(ds_name, monkeypatch):
     else:
         if ds_name.endswith("cgram2"):  # MFMA per-column Grams (k = 32), multi-chunk slot sums
             monkeypatch.setenv("OCFFM_CGRAM", "2")
+        if ds_name.endswith("pgram2"):  # pair Grams on the context field's side halves
+            monkeypatch.setenv("OCFFM_PGRAM", "2")
         ds = synth.kkbox(m=3000, n=4000, mean=20.0, seed=11, name="kk_det")
     runs = []
     for _ in range(2):
@@ -457,6 +470,7 @@ def test_speculative_update_bit_identical(monkeypatch):
     previous epoch, none, and fixed ones that hit, stop early and run past
     give bit-identical fp32 tables and CG logs over three epochs."""
     ds = synth.kkbox(m=3000, n=4000, mean=20.0, seed=11, name="kk_det")
+    monkeypatch.setenv("OCFFM_PGRAM", "2")  # the pair-Gram halves take the speculative update too
     runs = {}
     for cfg in ({"OCFFM_SPEC": "0"}, {}, {"OCFFM_SPEC_FIXED": "1"}, {"OCFFM_SPEC_FIXED": "2"},
                 {"OCFFM_SPEC_FIXED": "4"}):
@@ -485,7 +499,9 @@ def test_speculative_update_bit_identical(monkeypatch):
                                  {"OCFFM_NO_FOLD": "1"}, {"OCFFM_LAZY_BASE": "0"},
                                  {"OCFFM_SPEC_FIXED": "1"}, {"OCFFM_SPEC_FIXED": "2"}, {"OCFFM_SPEC": "0"},
                                  {"OCFFM_YSUM": "0"}, {"OCFFM_YTVIA": "0"}, {"OCFFM_HOT": "0"},
-                                 {"OCFFM_HOT": "3"}, {"OCFFM_EXACT_R2": "1"}, {"OCFFM_CCG": "0"}, {"OCFFM_CCG": "2"}])
+                                 {"OCFFM_HOT": "3"}, {"OCFFM_EXACT_R2": "1"}, {"OCFFM_CCG": "0"}, {"OCFFM_CCG": "2"},
+                                 {"OCFFM_CGP": "0"}, {"OCFFM_PGRAM": "2"}, {"OCFFM_PGRAM": "0"},
+                                 {"OCFFM_PGRAM": "2", "OCFFM_CGRAM": "2", "OCFFM_CCG": "2"}])
 def test_execution_variants_fp64(kk_small, monkeypatch, env):
     """Schedule knobs (id-field row fusion, segment length, CG look-ahead)
     change the kernels that run, never the result."""

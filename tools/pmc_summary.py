@@ -2,6 +2,7 @@
 
   python tools/pmc_summary.py stats  <kernel_stats.csv> <out.json>
   python tools/pmc_summary.py traffic <fetch_counter_collection.csv> <write_counter_collection.csv> <out.json>
+  python tools/pmc_summary.py variants <kernel_stats.csv> <fetch.csv> <write.csv> <regex> <out.json>
 
 `traffic` follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are
 collected in separate --pmc passes (kB units), FETCH_SIZE is doubled (gfx950
@@ -75,8 +76,43 @@ def traffic(fetch_csv, write_csv, out):
               f"write {v['write_bytes']/1e6:.2f})")
 
 
+def _variant(name):
+    """k_gd_cross_seg<float, 32, true, 2, false>(...) -> 'k_gd_cross_seg<float, 32, true, 2, false>'."""
+    m = re.search(r"(k_\w+<[^()]*>)", name)
+    return m.group(1) if m else re.sub(r"\(.*", "", name)
+
+
+def variants(stats_csv, fetch_csv, write_csv, regex, out):
+    """Per template instantiation (not per family) of the kernels matching
+    regex: calls, average duration (kernel trace) and FETCH_SIZE x2 +
+    WRITE_SIZE per launch (separate --pmc passes)."""
+    res = {}
+    for r in csv.DictReader(open(stats_csv)):
+        if not re.search(regex, r["Name"]):
+            continue
+        d = res.setdefault(_variant(r["Name"]), dict(calls=0, total_ns=0))
+        d["calls"] += int(r["Calls"])
+        d["total_ns"] += int(r["TotalDurationNs"])
+    for path, counter, key, mul in ((fetch_csv, "FETCH_SIZE", "fetch_bytes_x2", 2.0), (write_csv, "WRITE_SIZE",
+                                                                                         "write_bytes", 1.0)):
+        vals = defaultdict(list)
+        for r in csv.DictReader(open(path)):
+            if r.get("Counter_Name") == counter and re.search(regex, r["Kernel_Name"]):
+                vals[_variant(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+        for v, xs in vals.items():
+            res.setdefault(v, dict(calls=0, total_ns=0))[key] = mul * 1024 * sum(xs) / len(xs)
+    for v, d in res.items():
+        d["avg_us"] = d["total_ns"] / max(1, d["calls"]) / 1e3
+        d["bytes_per_launch"] = d.get("fetch_bytes_x2", 0.0) + d.get("write_bytes", 0.0)
+    json.dump(res, open(out, "w"), indent=1, sort_keys=True)
+    for k, v in sorted(res.items(), key=lambda kv: -kv[1]["total_ns"]):
+        print(f"{k:60s} calls {v['calls']:5d} avg {v['avg_us']:8.1f} us  PMC {v['bytes_per_launch'] / 1e6:8.1f} MB/launch")
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3])
+    elif sys.argv[1] == "variants":
+        variants(*sys.argv[2:7])
     else:
         traffic(sys.argv[2], sys.argv[3], sys.argv[4])

@@ -1,5 +1,5 @@
 """Per-kernel-family breakdown of epochs (HIP events on the solver stream).
-Usage: python tools/profile_epoch.py [fp32|fp64] [epochs] [kkbox|cfg5]"""
+Usage: python tools/profile_epoch.py [fp32|fp64] [epochs] [kkbox|cfg5|kdd12|outbrain]"""
 import json
 import os
 import sys
@@ -19,6 +19,9 @@ def main():
     if work == "cfg5":
         ds = synth.cfg5(m=int(os.environ.get("CFG5_ROWS", "2000000")))
         g = ocffm.problem_from_dataset(ds, precision=prec, with_test=False, k=64, self_side=False)
+    elif work in ("kdd12", "outbrain"):
+        ds = getattr(synth, work)()
+        g = ocffm.problem_from_dataset(ds, precision=prec, with_test=False)
     else:
         ds = synth.kkbox()
         g = ocffm.problem_from_dataset(ds, precision=prec, with_test=False)

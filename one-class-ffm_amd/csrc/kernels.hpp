@@ -999,7 +999,8 @@ template <typename real, int KP> struct TMma {
     }
   }
   // the tile of wave w (< NTW) for segments [base, base + SB) into Tl
-  static __device__ __forceinline__ void tile(uint64_t base, uint64_t nseg, const Seg *__restrict__ segs, int C,
+  static __device__ __forceinline__ void tile(uint64_t base, uint64_t nseg, const Seg *__restrict__ segs,
+                                              const uint32_t *__restrict__ sord, int C,
                                               const real *const *__restrict__ Ptabs, const real *Bt, real *Tl,
                                               int w, int lane) {
     const int tr = w % TR, tc = w / TR;
@@ -1008,7 +1009,7 @@ template <typename real, int KP> struct TMma {
     bool have = false;
     uint64_t row = 0;
     if (si < nseg) {
-      const Seg s = segs[si];
+      const Seg s = segs[sord ? (uint64_t)sord[si] : si];
       have = seg_first(s);
       row = s.row;
     }
@@ -1107,7 +1108,8 @@ __global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_GD_OCC64 : OCFFM_G
                                                         const real *__restrict__ dxs,
                                                         const uint32_t *__restrict__ perm,
                                                         const real *__restrict__ Tpre,
-                                                        const real *__restrict__ ytv) {
+                                                        const real *__restrict__ ytv,
+                                                        const uint32_t *__restrict__ sord) {
   using G = Geo<real, KP>;
   using PP = PosPass<real, KP, sizeof(real) == 8 ? OCFFM_GD_GB64 : (BM == BM_ENTER ? OCFFM_GD_GB : OCFFM_GD_GB_IN)>;
   // TP: T_i precomputed by k_rows_T (one row load; no M in LDS)
@@ -1277,14 +1279,22 @@ __global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_GD_OCC64 : OCFFM_G
     // before the next iteration rewrites the tile
     const int wv = threadIdx.x >> 6;
     for (uint64_t base = (uint64_t)blockIdx.x * TMM::SB; base < nseg; base += (uint64_t)gridDim.x * TMM::SB) {
-      if (!PRB && wv < TMM::NTW) TMM::tile(base, nseg, segs, C, Ptabs, Ms, Tl, wv, lane);
+      if (!PRB && wv < TMM::NTW) TMM::tile(base, nseg, segs, sord, C, Ptabs, Ms, Tl, wv, lane);
       __syncthreads();
       const uint64_t s = base + (uint64_t)wv * G::NSG + sg;
-      if (s < nseg) vst<real>(h + s * KP + li * G::VE, body(segs[s]));
+      if (s < nseg) {
+        const uint64_t sx = sord ? (uint64_t)sord[s] : s;
+        vst<real>(h + sx * KP + li * G::VE, body(segs[sx]));
+      }
       __syncthreads();
     }
   } else {
-    for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) vst<real>(h + s * KP + li * G::VE, body(segs[s]));
+    // sord (optional): processing order of the segments (longest first, as
+    // in k_hs_cross_seg); h stays in segment order
+    for (uint64_t s = wave * G::NSG + sg; s < nseg; s += nwaves * G::NSG) {
+      const uint64_t sx = sord ? (uint64_t)sord[s] : s;
+      vst<real>(h + sx * KP + li * G::VE, body(segs[sx]));
+    }
   }
 }
 
@@ -2171,7 +2181,8 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
                                                         const uint32_t *__restrict__ segd,
                                                         const real *__restrict__ segx,
                                                         const uint32_t *__restrict__ hot_seg,
-                                                        const real *__restrict__ hotG) {
+                                                        const real *__restrict__ hotG,
+                                                        const uint32_t *__restrict__ sord) {
   using G = Geo<real, KP>;
   // gathers per round (32: one round per <= 32-positive segment)
   using PP = PosPass<real, KP, sizeof(real) == 8 ? OCFFM_HS_GB64 : OCFFM_HS_GB>;
@@ -2237,32 +2248,32 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
   };
   // Grid-stride over segments with the next segment's descriptor (and its
   // node) in flight while the current one is gathered.
+  // sord (optional): the order in which the subgroups take the segments
+  // (longest first: a wave's subgroups then walk similar lengths, so fewer
+  // absent slots pass through the gather rounds); h stays in segment order
   const uint64_t stride = nwaves * G::NSG;
   uint64_t s = wave * G::NSG + sg;
   Seg nxt{0u, 0u, 0, 0};
   uint32_t nd = 0, nh = HOT_NONE;
+  uint64_t nsx = 0;
   real nx = 0;
-  if (s < nseg) {
-    nxt = segs[s];
+  auto fetch = [&](uint64_t q) {
+    nsx = sord ? (uint64_t)sord[q] : q;
+    nxt = segs[nsx];
     if (segd) {
-      nd = segd[s];
-      nx = segx[s];
+      nd = segd[nsx];
+      nx = segx[nsx];
     }
-    if (hot_seg) nh = hot_seg[s];
-  }
+    if (hot_seg) nh = hot_seg[nsx];
+  };
+  if (s < nseg) fetch(s);
   for (; s < nseg; s += stride) {
     const Seg sgm = nxt;
     const uint32_t d1 = nd, hs = nh;
     const real x1 = nx;
-    if (s + stride < nseg) {
-      nxt = segs[s + stride];
-      if (segd) {
-        nd = segd[s + stride];
-        nx = segx[s + stride];
-      }
-      if (hot_seg) nh = hot_seg[s + stride];
-    }
-    vst<real>(h + s * KP + li * G::VE, seg_out(sgm, d1, x1, hs));
+    const uint64_t sx = nsx;
+    if (s + stride < nseg) fetch(s + stride);
+    vst<real>(h + sx * KP + li * G::VE, seg_out(sgm, d1, x1, hs));
   }
 }
 

@@ -194,6 +194,7 @@ template <typename real> struct DevSide {
   DevBuf<real> s;         // sa or sb
   uint64_t nseg = 0;      // positive segments (kernels.hpp: Seg)
   DevBuf<Seg> segs;
+  DevBuf<uint32_t> sord;  // the cross row passes' processing order of the segments (longest first)
   DevBuf<uint32_t> segptr;
   // Hot rows (kernels.hpp k_hot_gram*): rows with >= hot_min positives whose
   // cross-half Hessian-vector rows read a k x k Gram of their partner rows
@@ -492,6 +493,8 @@ template <typename real> class Problem final : public ProblemBase {
       for (uint32_t fi = 0; fi < sd->F.size(); fi++)
         if (ccg_field_all(*sd->F[fi], *sd, sd == &U_, fi, U)) ccg_setup(*sd->F[fi], *sd);
     if (io_mode_ != 0 && comm_.active() && (comm_.nranks > 1 || io_mode_ == 2) && C_ > 0) io_setup(U, V);
+    build_sorder(U_);
+    build_sorder(V_);
     // pair Grams of the side halves of low-cardinality multi-node fields
     // (one GPU: every rank would otherwise have to agree on its local shard's
     // pair count, and the multi-rank path has its own partial-sum protocol)
@@ -1945,7 +1948,7 @@ template <typename real> class Problem final : public ProblemBase {
                 (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, h.partner->bias.p, w_,
                 r_, h_.p, (uint64_t)h.partner->R, cur, drow, dxs, (const uint32_t *)own.perm.p,
                 TP ? (const real *)Tpre_.p : (const real *)nullptr,
-                via ? (const real *)h.partner->yt.p : (const real *)nullptr);
+                via ? (const real *)h.partner->yt.p : (const real *)nullptr, sord(own));
           };
           if constexpr (std::is_same<real, float>::value && (KP == 32 || KP == 64) && !ML) {
             if (tp) {
@@ -1968,7 +1971,7 @@ template <typename real> class Problem final : public ProblemBase {
                    0, own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
                    (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, h.partner->bias.p, w_,
                    r_, h_.p, (uint64_t)h.partner->R, cur, drow, dxs, (const uint32_t *)own.perm.p,
-                   (const real *)nullptr, via ? (const real *)h.partner->yt.p : (const real *)nullptr);
+                   (const real *)nullptr, via ? (const real *)h.partner->yt.p : (const real *)nullptr, sord(own));
           };
           prof_launch("gd_probe", bytes, [&] {
             if (!cur) probe(std::integral_constant<int, BM_FULL>());
@@ -2401,7 +2404,9 @@ template <typename real> class Problem final : public ProblemBase {
 
   // ---- pair Grams (kernels.hpp k_pg_step; OCFFM_PGRAM: 0 off, 1 where
   // the gate below passes, 2 wherever the structure allows)
-  int pgram_mode_ = std::getenv("OCFFM_PGRAM") ? std::atoi(std::getenv("OCFFM_PGRAM")) : 1;
+  // (default off: measured 5.37 -> 5.63 ms per kkbox epoch against the
+  // column-block feature pass)
+  int pgram_mode_ = std::getenv("OCFFM_PGRAM") ? std::atoi(std::getenv("OCFFM_PGRAM")) : 0;
   static constexpr uint64_t PG_FIN1 = 1024;  // k_pg_step finalises in its last block up to this many features
   DevBuf<real> pgt_;                          // its per-(feature, block) partial slots
   bool pgram(const HalfCtx &h) const { return !h.cross && h.F->pg; }
@@ -3000,7 +3005,7 @@ template <typename real> class Problem final : public ProblemBase {
                    io.nseg, io.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, io.ycol.p, (const real *)Pg_.p,
                    (uint64_t)comm_.nranks * io_cu_, ct ? (const real *)nullptr : (const real *)qtqg_.p, w_, h_.p,
                    run, Rv_.p, Hv_.p, st_.p, it, io.segd.p, io.segx.p, (const uint32_t *)nullptr,
-                   (const real *)nullptr);
+                   (const real *)nullptr, (const uint32_t *)nullptr);
           };
           if (lds) go(std::true_type());
           else go(std::false_type());
@@ -3060,6 +3065,32 @@ template <typename real> class Problem final : public ProblemBase {
                run_host_dev_ + MAXCG + 3);
       });
     });
+  }
+
+  // Processing order of a side's segments for the cross row passes
+  // (k_gd_cross_seg, k_hs_cross_seg): by length, longest first, stable (a
+  // counting sort of the lengths <= seg_len_).  A wave's subgroups take
+  // consecutive entries, so they walk segments of similar length and the
+  // gather rounds carry fewer absent slots (item rows: median ~10 positives
+  // in 32-slot rounds).  Opt-in (OCFFM_SORDER=1): measured slower, 5.40 ->
+  // 5.58 ms per kkbox epoch (gd_cross_row 72.8 -> 81.1 us: the MFMA T tile's
+  // rows and the h stores lose their contiguity).
+  bool sorder_on_ = std::getenv("OCFFM_SORDER") && std::atoi(std::getenv("OCFFM_SORDER")) != 0;
+  const uint32_t *sord(const DevSide<real> &sd) const { return sorder_on_ && sd.sord.p ? sd.sord.p : nullptr; }
+  void build_sorder(DevSide<real> &sd) {
+    if (!sorder_on_ || sd.nseg == 0 || sd.nseg >= (1ull << 32)) return;
+    std::vector<Seg> sg(sd.nseg);
+    HIPCHK(hipMemcpy(sg.data(), sd.segs.p, sd.nseg * sizeof(Seg), hipMemcpyDeviceToHost));
+    // key k = L - len in [0, L] (longest first); bucket starts by an
+    // exclusive prefix sum over the L + 1 keys
+    const uint64_t L = seg_len_ + 1;
+    auto key = [&](const Seg &x) { return L - std::min<uint64_t>(L, (uint64_t)(x.e - x.b)); };
+    std::vector<uint64_t> start(L + 2, 0);
+    for (const Seg &x : sg) start[key(x) + 1]++;
+    for (uint64_t k = 0; k <= L; k++) start[k + 1] += start[k];
+    std::vector<uint32_t> ord(sd.nseg);
+    for (uint64_t q = 0; q < sd.nseg; q++) ord[start[key(sg[q])]++] = (uint32_t)q;
+    sd.sord.upload(ord);
   }
 
   void hv_product(HalfCtx &h, int it) {
@@ -3126,7 +3157,7 @@ template <typename real> class Problem final : public ProblemBase {
                    own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.ycol.p, h.Q1, (uint64_t)h.partner->R,
                    coltau(h) ? (const real *)nullptr : (const real *)qtq_, w_, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
                    F.segd.p, F.segx.p, hot(h) ? (const uint32_t *)own.hot_seg.p : (const uint32_t *)nullptr,
-                   (const real *)hotG_.p);
+                   (const real *)hotG_.p, sord(own));
           };
           prof_launch("hs_cross_row", bytes, [&] {
             if (lds) go(std::true_type());

@@ -379,9 +379,10 @@ __device__ __forceinline__ vec_t<real> sg_reduce_scatter(real (&u)[KP], int li) 
 // zero rows), so a 32-position segment costs 1 + 32/GB latency rounds
 // instead of one per position.
 constexpr uint32_t POS_NONE = 0xffffffffu;
-template <typename real, int KP, int GB_ = 8> struct PosPass {
+template <typename real, int KP, int GB_ = 8, int PW_ = 32> struct PosPass {
   using G = Geo<real, KP>;
-  static constexpr int PW = G::LPR > 32 ? G::LPR : 32;
+  // positions per pass (PW_: 32, or 16 for sides whose segments are short)
+  static constexpr int PW = G::LPR > PW_ ? G::LPR : PW_;
   static constexpr int UT = PW / G::LPR;
   static constexpr int GB = GB_ < PW ? GB_ : PW;  // gathers per round
   static constexpr uint32_t ROWB = KP * sizeof(real);
@@ -1015,7 +1016,10 @@ template <typename real, int KP> struct TMma {
     }
     const int nch = C * KP / 16;
     if constexpr (std::is_same<real, float>::value) {
-      f4v acc = {0.f, 0.f, 0.f, 0.f};
+      // GR independent accumulators (chunk u of a group into acc[u]): the
+      // chain of C KP / 4 dependent MFMAs (40-cycle accumulator latency) cut
+      // into GR interleaved ones, summed at the end
+      f4v acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
       constexpr int GR = 4;  // chunks per load group (two groups in flight)
       f4v a[2][GR];
       auto load = [&](auto SB_, int j0) {
@@ -1035,7 +1039,8 @@ template <typename real, int KP> struct TMma {
           if (j < nch) {
             const f4v b = *reinterpret_cast<const f4v *>(Bt + ((4 * j + q) * KP + tc * 16 + m) * 4);
 #pragma unroll
-            for (int s = 0; s < 4; s++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[sb][u][s], b[s], acc, 0, 0, 0);
+            for (int s = 0; s < 4; s++)
+              acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[sb][u][s], b[s], acc[u], 0, 0, 0);
           }
         }
       };
@@ -1047,8 +1052,9 @@ template <typename real, int KP> struct TMma {
         load(std::integral_constant<int, 0>(), j0 + 2 * GR);
         mma(std::integral_constant<int, 1>(), j0 + GR);
       }
+      const f4v t = (acc[0] + acc[1]) + (acc[2] + acc[3]);
 #pragma unroll
-      for (int r = 0; r < 4; r++) Tl[(tr * 16 + drow(lane, r)) * KP + tc * 16 + m] = acc[r];
+      for (int r = 0; r < 4; r++) Tl[(tr * 16 + drow(lane, r)) * KP + tc * 16 + m] = t[r];
     } else {
       typedef double d4 __attribute__((ext_vector_type(4)));
       d4 acc = {0.0, 0.0, 0.0, 0.0};
@@ -2168,7 +2174,7 @@ __global__ __launch_bounds__(BLOCK) void k_cg_cgram(uint64_t D, const real *__re
 // + [first] w phi_i QTQ, phi_i = X_i p  (hs_cross row body, ffm.cpp:715-738;
 // tau = X_i (V QTQ) = phi_i QTQ).  QTQ staged in LDS; phi_i's components
 // are broadcast by DPP for the k x k product (sg_vecmat).
-template <typename real, int KP, bool MLDS>
+template <typename real, int KP, bool MLDS, int PW_ = 32>
 __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                         const int64_t *__restrict__ xptr,
                                                         const uint32_t *__restrict__ xidx,
@@ -2184,8 +2190,10 @@ __global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t n
                                                         const real *__restrict__ hotG,
                                                         const uint32_t *__restrict__ sord) {
   using G = Geo<real, KP>;
-  // gathers per round (32: one round per <= 32-positive segment)
-  using PP = PosPass<real, KP, sizeof(real) == 8 ? OCFFM_HS_GB64 : OCFFM_HS_GB>;
+  // gathers per round (32: one round per <= 32-positive segment); PW_ = 16
+  // for sides whose segments are nearly all short (outbrain's users: ~1
+  // positive each), so a round carries fewer absent slots
+  using PP = PosPass<real, KP, sizeof(real) == 8 ? OCFFM_HS_GB64 : OCFFM_HS_GB, PW_>;
   const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real));
   if (run && !*run) return;
   const bool upd = st && it > 1;

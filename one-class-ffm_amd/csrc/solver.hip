@@ -195,6 +195,7 @@ template <typename real> struct DevSide {
   uint64_t nseg = 0;      // positive segments (kernels.hpp: Seg)
   DevBuf<Seg> segs;
   DevBuf<uint32_t> sord;  // the cross row passes' processing order of the segments (longest first)
+  bool short_segs = false;  // >= 99 % of the segments hold <= 16 positives (k_hs_cross_seg's 16-position pass)
   DevBuf<uint32_t> segptr;
   // Hot rows (kernels.hpp k_hot_gram*): rows with >= hot_min positives whose
   // cross-half Hessian-vector rows read a k x k Gram of their partner rows
@@ -495,6 +496,8 @@ template <typename real> class Problem final : public ProblemBase {
     if (io_mode_ != 0 && comm_.active() && (comm_.nranks > 1 || io_mode_ == 2) && C_ > 0) io_setup(U, V);
     build_sorder(U_);
     build_sorder(V_);
+    seg_shape(U_);
+    seg_shape(V_);
     // pair Grams of the side halves of low-cardinality multi-node fields
     // (one GPU: every rank would otherwise have to agree on its local shard's
     // pair count, and the multi-rank path has its own partial-sum protocol)
@@ -504,8 +507,8 @@ template <typename real> class Problem final : public ProblemBase {
     // T pre-pass rows: the larger side that takes the pre-pass (tpre() also
     // bounds R for 32-bit buffer offsets, so test each side on its own)
     uint64_t tR = 0;
-    for (const uint64_t R : {U_.R, V_.R})
-      if (tpre(R)) tR = std::max(tR, R);
+    for (const DevSide<real> *sd : {&U_, &V_})
+      if (tpre(sd->R, sd->npos)) tR = std::max(tR, sd->R);
     if (tR) Tpre_.alloc(tR * kp_);
   }
 
@@ -1926,7 +1929,7 @@ template <typename real> class Problem final : public ProblemBase {
         const bool via = ytvia_ && cur && !enter;
         // T_i = sum_c P_c[i] M_c on MFMA ahead of the pass (k_rows_T), where
         // the C Grams do not fit the pass's LDS (or OCFFM_TPRE=1)
-        const bool tp = tpre(own.R);
+        const bool tp = tpre(own.R, own.npos);
         if (tp) {
           if constexpr (std::is_same<real, float>::value && (KP == 32 || KP == 64)) {
             const uint64_t nb = (own.R + RowsT<KP>::ROWS - 1) / RowsT<KP>::ROWS;
@@ -2671,8 +2674,9 @@ template <typename real> class Problem final : public ProblemBase {
   // the half's field.  mode 0/1 finalise (gradient / Hessian-vector of CG
   // iteration it); mode 2 stores the column sums into acc_.
   // Column-block feature pass (kernels.hpp k_feat_col): a field with few,
-  // heavy columns (at most 4,096 columns of 64 entries or more on average),
-  // not owned (its CSC's unowned columns have no jobs), no column tau.
+  // heavy columns (at most 4,096 columns of 64 entries or more on average,
+  // none longer than 4,096), not owned (its CSC's unowned columns have no
+  // jobs), no column tau.
   int feat_col_mode_ = std::getenv("OCFFM_FEATCOL") ? std::atoi(std::getenv("OCFFM_FEATCOL")) : 1;
   bool feat_col(HalfCtx &h, bool seg, int mode) {
     DevField<real> &F = *h.F;
@@ -2700,7 +2704,12 @@ template <typename real> class Problem final : public ProblemBase {
             cp[c + 1] = last[c];
           }
         }
-        if (ok && (uint64_t)cp[F.D] == ent) {
+        // one block walks a whole column: only where no column is long (at
+        // most 16 rounds of 256 entries; outbrain's platform columns of
+        // ~83 k rows took 587 us per step this way, the job-based pass ~50)
+        int64_t cmax = 0;
+        for (uint64_t c = 0; c < F.D; c++) cmax = std::max<int64_t>(cmax, cp[c + 1] - cp[c]);
+        if (ok && (uint64_t)cp[F.D] == ent && (feat_col_mode_ == 2 || cmax <= 4096)) {
           F.fcptr[ix].upload(cp);
           F.fcol[ix] = 1;
         }
@@ -3093,6 +3102,22 @@ template <typename real> class Problem final : public ProblemBase {
     sd.sord.upload(ord);
   }
 
+  // Segment length profile of a side (host, once): short_segs when at
+  // least 99 % of its segments hold at most 16 positives (outbrain's users:
+  // ~1 positive per row), where k_hs_cross_seg's passes of 16 positions
+  // carry half the absent slots of the 32-position pass (OCFFM_SHORTPASS=0:
+  // always 32).
+  bool shortpass_on_ = !std::getenv("OCFFM_SHORTPASS") || std::atoi(std::getenv("OCFFM_SHORTPASS")) != 0;
+  void seg_shape(DevSide<real> &sd) {
+    sd.short_segs = false;
+    if (!shortpass_on_ || sd.nseg == 0) return;
+    std::vector<Seg> sg(sd.nseg);
+    HIPCHK(hipMemcpy(sg.data(), sd.segs.p, sd.nseg * sizeof(Seg), hipMemcpyDeviceToHost));
+    uint64_t small = 0;
+    for (const Seg &x : sg) small += (x.e - x.b) <= 16 ? 1 : 0;
+    sd.short_segs = (double)small >= 0.99 * (double)sd.nseg;
+  }
+
   void hv_product(HalfCtx &h, int it) {
     DevSide<real> &own = *h.own;
     const int *run = &st_.p->run[it];
@@ -3153,11 +3178,22 @@ template <typename real> class Problem final : public ProblemBase {
                                (double)own.npos * 4 + (double)h.partner->R * KP * rs + (double)own.R * KP * rs;
           auto go = [&](auto ml) {
             constexpr bool ML = decltype(ml)::value;
-            launch(k_hs_cross_seg<real, KP, ML>, grid_for(own.nseg, 4 * Gm::NSG, hs_blocks_), BLOCK, smem, own.nseg,
-                   own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.ycol.p, h.Q1, (uint64_t)h.partner->R,
-                   coltau(h) ? (const real *)nullptr : (const real *)qtq_, w_, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
-                   F.segd.p, F.segx.p, hot(h) ? (const uint32_t *)own.hot_seg.p : (const uint32_t *)nullptr,
-                   (const real *)hotG_.p, sord(own));
+            auto go2 = [&](auto pw) {
+              constexpr int PW = decltype(pw)::value;
+              launch(k_hs_cross_seg<real, KP, ML, PW>, grid_for(own.nseg, 4 * Gm::NSG, hs_blocks_), BLOCK, smem,
+                     own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.ycol.p, h.Q1,
+                     (uint64_t)h.partner->R, coltau(h) ? (const real *)nullptr : (const real *)qtq_, w_, h_.p, run,
+                     Rv_.p, Hv_.p, st_.p, it, F.segd.p, F.segx.p,
+                     hot(h) ? (const uint32_t *)own.hot_seg.p : (const uint32_t *)nullptr, (const real *)hotG_.p,
+                     sord(own));
+            };
+            if constexpr (Gm::LPR <= 16) {
+              if (own.short_segs) {
+                go2(std::integral_constant<int, 16>());
+                return;
+              }
+            }
+            go2(std::integral_constant<int, 32>());
           };
           prof_launch("hs_cross_row", bytes, [&] {
             if (lds) go(std::true_type());
@@ -3423,11 +3459,18 @@ template <typename real> class Problem final : public ProblemBase {
   DevBuf<real> Tpre_;
   // grid cap: one 512-thread block per CU (128 KB of LDS each)
   unsigned tpre_blocks_ = std::getenv("OCFFM_TPRE_BLOCKS") ? (unsigned)std::max(1, std::atoi(std::getenv("OCFFM_TPRE_BLOCKS"))) : 256;
-  bool tpre(uint64_t R) const {
+  // T_i as an MFMA pre-pass (k_rows_T): where the C Grams do not fit the
+  // gradient pass's LDS, or where the rows carry few positives (< 4 per row
+  // on average: the pass is then mostly its T_i work; outbrain's 250 k
+  // users with ~1.2 each: gd_cross_row 193 -> 61 us + rows_T 71 us), or
+  // OCFFM_TPRE=1
+  bool tpre(uint64_t R, uint64_t npos) const {
     const bool big = (size_t)C_ * kp_ * kp_ * sizeof(real) > 64 * 1024;
-    return (tpre_on_ || big) && std::is_same<real, float>::value && (kp_ == 32 || kp_ == 64) && C_ >= 1 && R > 0 &&
-           (uint64_t)R * kp_ * sizeof(real) < 0xffffff00ull && !no_mfma_;
+    const bool few = tpre_few_ && R >= 65536 && npos < 4 * R;
+    return (tpre_on_ || big || few) && std::is_same<real, float>::value && (kp_ == 32 || kp_ == 64) && C_ >= 1 &&
+           R > 0 && (uint64_t)R * kp_ * sizeof(real) < 0xffffff00ull && !no_mfma_;
   }
+  bool tpre_few_ = !std::getenv("OCFFM_TPRE_FEW") || std::atoi(std::getenv("OCFFM_TPRE_FEW")) != 0;
   DevBuf<real> ysum_;
   void ysum_dirty() { ysum_ok_[0] = ysum_ok_[1] = false; }
   // hot rows: positives per row from which a cross half reads a per-row

@@ -28,6 +28,8 @@ FAMILY = [  # (regex on the demangled kernel name, family as named by the librar
     (r"k_apply", "apply_step"), (r"k_rowdot_multi", "rowdot_multi"), (r"k_colsum_multi", "aggregates"),
     (r"k_cg_step", "cg_step"), (r"k_cg_r2", "cg_r2"), (r"k_hot_gram|k_gram_add_tau|k_hot_slot_sum", "ccg_build"),
     (r"k_hot_seg", "hot_seg"), (r"k_mask_rows", "mask_rows"), (r"k_sgd<", "k_sgd"), (r"k_phi<", "k_phi"),
+    (r"k_feat_col<\w+, \d+, 1\b", "feat_hv"), (r"k_feat_col<\w+, \d+, 0\b", "feat_grad"),
+    (r"k_feat_col<\w+, \d+, 2\b", "csc_scatter"), (r"k_cg_cgram", "cg_cgram"), (r"k_pg_step", "pg_step"),
 ]
 
 

@@ -176,7 +176,7 @@ template <typename real> __device__ __forceinline__ vec_t<real> vsplat(real x) {
 // ------------------------------------------------------ lane exchange ---
 // DPP lane moves run on the VALU (no LDS-pipe ds_bpermute).  Controls:
 // quad_perm 0x00-0xff, row_shl:n 0x100+n, row_shr:n 0x110+n,
-// row_mirror 0x140, row_half_mirror 0x141.
+// row_mirror 0x140, row_half_mirror 0x141, row_newbcast:n 0x150+n (gfx950).
 template <int CTRL> __device__ __forceinline__ uint32_t dpp32(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
 }
@@ -224,6 +224,8 @@ template <int LPR, int SRC, typename T> __device__ __forceinline__ T sg_bcast(T 
       const T b = dpp<0x104>(a);  // row_shl:4: the lower quad takes the upper one's
       return (li & 4) ? a : b;
     }
+  } else if constexpr (LPR == 16) {
+    return dpp<0x150 + SRC>(x);  // row_newbcast: lane SRC of each 16-lane row (no LDS-pipe bpermute)
   } else {
     return __shfl(x, (int)((threadIdx.x & 63) & ~(LPR - 1)) + SRC, 64);
   }
@@ -545,15 +547,17 @@ template <typename real, int KP>
 __device__ __forceinline__ vec_t<real> cg_dir_at(const real *__restrict__ P, const real *__restrict__ Rv,
                                                  const real *__restrict__ Hv, real alpha, real beta, bool upd,
                                                  size_t off) {
-  // branch-free: the three loads go out together (a select, not a branch,
-  // picks the formula; without upd the R/Hp rows are read but unused)
+  // upd is uniform over a launch: the three loads go out together, or only
+  // the p row (the first CG step).  (Round 5: forming p_it once per step in
+  // its own pass, so that the row passes read one row per node reference,
+  // measured a net loss on every shape: the ~4.5 us launch outweighed what
+  // hs_cross / hs_side saved, ~2-5 us per launch even at outbrain's three
+  // nodes per ~1-positive row.)
+  if (!upd) return vld<real>(P + off);
   const vec_t<real> p = vld<real>(P + off), r = vld<real>(Rv + off), hp = vld<real>(Hv + off);
-  const vec_t<real> u = (r - vsplat<real>(alpha) * hp) + vsplat<real>(beta) * p;
-  vec_t<real> o;
-#pragma unroll
-  for (int e = 0; e < VT<real>::N; e++) o[e] = upd ? u[e] : p[e];
-  return o;
+  return (r - vsplat<real>(alpha) * hp) + vsplat<real>(beta) * p;
 }
+
 
 // ------------------------------------------------ column finalisation ---
 // Arguments of the finalisation of a D x k gradient / Hessian-vector column.

@@ -28,6 +28,7 @@
 #include <string>
 #include <thread>
 #include <tuple>
+#include <unordered_map>
 #include <type_traits>
 #include <vector>
 
@@ -1527,6 +1528,19 @@ template <typename real> class Problem final : public ProblemBase {
   // pair, the dispatch packet itself carries them (hipExtLaunchKernel: start
   // on the first dispatch of the armed region, stop after each), so the
   // recorded time is the kernels' own, as rocprofv3's kernel trace sees it.
+  // Blocks of kernel k (BLOCK threads, smem bytes) resident on the whole
+  // GPU at once (the occupancy API's per-CU count x CUs; cached per kernel).
+  std::unordered_map<const void *, unsigned> resident_;
+  template <typename... KArgs> unsigned resident(void (*k)(KArgs...), size_t smem) {
+    const void *key = reinterpret_cast<const void *>(k);
+    auto it = resident_.find(key);
+    if (it != resident_.end()) return it->second;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, key, BLOCK, smem) != hipSuccess || nb <= 0) nb = 1;
+    const unsigned r = (unsigned)nb * std::max(1u, ncu_);
+    resident_[key] = r;
+    return r;
+  }
   template <typename... KArgs, typename... A>
   void launch(void (*k)(KArgs...), dim3 grid, dim3 block, size_t smem, A... a) {
     static_assert(sizeof...(KArgs) == sizeof...(A), "kernel argument count");
@@ -1946,8 +1960,12 @@ template <typename real> class Problem final : public ProblemBase {
             constexpr bool TP = decltype(tpc)::value;
             // (with T on the matrix cores the block also holds its T tile)
             constexpr bool TM = ML && !TP && TMma<real, KP>::OK;
-            launch(k_gd_cross_seg<real, KP, ML, BM, TP>, grid_for(own.nseg, 4 * Gm::NSG, gd_blocks_), BLOCK,
-                TP ? 0 : (ML ? msz + (TM ? TMma<real, KP>::tile_bytes() : 0) : 0), own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
+            // one resident wave of blocks (OCFFM_GD_FILL): the grid-stride
+            // loop then has no partial last wave of blocks
+            const size_t gsm = TP ? 0 : (ML ? msz + (TM ? TMma<real, KP>::tile_bytes() : 0) : 0);
+            unsigned grid = grid_for(own.nseg, 4 * Gm::NSG, gd_blocks_);
+            if (gd_fill_) grid = std::min(grid, resident(k_gd_cross_seg<real, KP, ML, BM, TP>, gsm));
+            launch(k_gd_cross_seg<real, KP, ML, BM, TP>, grid, BLOCK, gsm, own.nseg, own.segs.p, own.ycol.p, own.yt.p, h.Q1, (int)C_,
                 (const real *const *)(tabs_.p + (h.user ? 0 : C_)), M_.p, sums_.p, own.bias.p, h.partner->bias.p, w_,
                 r_, h_.p, (uint64_t)h.partner->R, cur, drow, dxs, (const uint32_t *)own.perm.p,
                 TP ? (const real *)Tpre_.p : (const real *)nullptr,
@@ -2758,7 +2776,10 @@ template <typename real> class Problem final : public ProblemBase {
       const double vecs = mode == 2 ? 1 : (mode == 0 ? 5 : (it > 1 ? 8 : 3));
       const double bytes = (double)ent * (4 + rs) + (double)ent * KP * rs + (double)njw * Gm::NSG * sizeof(Job) +
                            (double)h.D * KP * rs * vecs;
-      const unsigned grid = (unsigned)std::min<uint64_t>((njw + 3) / 4, feat_blocks_);  // grid-stride: fewer tickets
+      const unsigned grid0 = (unsigned)std::min<uint64_t>((njw + 3) / 4, feat_blocks_);  // grid-stride: fewer tickets
+      // at most one resident wave of blocks (OCFFM_FEAT_FILL): fp64's
+      // register count holds fewer blocks per CU than the fp32 cap assumes
+      auto fill = [&](auto k, size_t sm) { return feat_fill_ ? std::min(grid0, resident(k, sm)) : grid0; };
       Fin<real> fin = make_fin(h, it);
       fin.hdots = seg ? F.shdots.p : F.hdots.p;
       fin.nhd = (uint32_t)(seg ? F.snslot : F.nslot);
@@ -2770,28 +2791,32 @@ template <typename real> class Problem final : public ProblemBase {
       const char *name = mode == 2 ? "csc_scatter" : (mode == 0 ? "feat_grad" : "feat_hv");
       const real *nq = nullptr;
       prof_launch(name, bytes, [&] {
+        constexpr size_t tq = (size_t)KP * KP * sizeof(real);
         if (mode == 0) {
-          launch(k_feat<real, KP, 0>, grid, BLOCK, 0, njw, jobs, crow, cval, hb, hbytes, wpart_.p, wpart_.bytes(), fin, nq);
+          launch(k_feat<real, KP, 0>, fill(k_feat<real, KP, 0>, 0), BLOCK, 0, njw, jobs, crow, cval, hb, hbytes,
+                 wpart_.p, wpart_.bytes(), fin, nq);
         } else if (mode == 1) {
-          if constexpr ((size_t)KP * KP * sizeof(real) <= COLTAU_LDS) {
+          if constexpr (tq <= COLTAU_LDS) {
             if (coltau(h)) {
               fin.xsq = F.xsq.p;
-              launch(k_feat<real, KP, 1, JOB_ENT, true>, grid, BLOCK, (size_t)KP * KP * sizeof(real), njw, jobs, crow,
-                     cval, hb, hbytes, wpart_.p, wpart_.bytes(), fin, (const real *)qtq_);
+              launch(k_feat<real, KP, 1, JOB_ENT, true>, fill(k_feat<real, KP, 1, JOB_ENT, true>, tq), BLOCK, tq, njw,
+                     jobs, crow, cval, hb, hbytes, wpart_.p, wpart_.bytes(), fin, (const real *)qtq_);
               return;
             }
           }
-          launch(k_feat<real, KP, 1>, grid, BLOCK, 0, njw, jobs, crow, cval, hb, hbytes, wpart_.p, wpart_.bytes(), fin, nq);
+          launch(k_feat<real, KP, 1>, fill(k_feat<real, KP, 1>, 0), BLOCK, 0, njw, jobs, crow, cval, hb, hbytes,
+                 wpart_.p, wpart_.bytes(), fin, nq);
         } else {
-          if constexpr ((size_t)KP * KP * sizeof(real) <= COLTAU_LDS) {
+          if constexpr (tq <= COLTAU_LDS) {
             if (coltau(h) && it > 0) {
               fin.xsq = F.xsq.p;
-              launch(k_feat<real, KP, 2, JOB_ENT, true>, grid, BLOCK, (size_t)KP * KP * sizeof(real), njw, jobs, crow,
-                     cval, hb, hbytes, wpart_.p, wpart_.bytes(), fin, (const real *)qtq_);
+              launch(k_feat<real, KP, 2, JOB_ENT, true>, fill(k_feat<real, KP, 2, JOB_ENT, true>, tq), BLOCK, tq, njw,
+                     jobs, crow, cval, hb, hbytes, wpart_.p, wpart_.bytes(), fin, (const real *)qtq_);
               return;
             }
           }
-          launch(k_feat<real, KP, 2>, grid, BLOCK, 0, njw, jobs, crow, cval, hb, hbytes, wpart_.p, wpart_.bytes(), fin, nq);
+          launch(k_feat<real, KP, 2>, fill(k_feat<real, KP, 2>, 0), BLOCK, 0, njw, jobs, crow, cval, hb, hbytes,
+                 wpart_.p, wpart_.bytes(), fin, nq);
         }
       });
     });
@@ -3534,6 +3559,8 @@ template <typename real> class Problem final : public ProblemBase {
   bool lazy_base_ = !std::getenv("OCFFM_LAZY_BASE") || std::atoi(std::getenv("OCFFM_LAZY_BASE")) != 0;
   // grid cap of the cross gradient pass (each block stages the C aggregates M in LDS)
   unsigned gd_blocks_ = std::getenv("OCFFM_GD_BLOCKS") ? (unsigned)std::atoi(std::getenv("OCFFM_GD_BLOCKS")) : 2048u;
+  bool gd_fill_ = !std::getenv("OCFFM_GD_FILL") || std::atoi(std::getenv("OCFFM_GD_FILL")) != 0;
+  bool feat_fill_ = !std::getenv("OCFFM_FEAT_FILL") || std::atoi(std::getenv("OCFFM_FEAT_FILL")) != 0;
   bool want_g_ = false;  // grad(): the gradient finalisation also stores G
   const real *qtq_ = nullptr;  // this cross half's Q^T Q: a slot of M_
   DevBuf<unsigned> tick_;

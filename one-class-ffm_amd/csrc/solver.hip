@@ -1541,6 +1541,12 @@ template <typename real> class Problem final : public ProblemBase {
     resident_[key] = r;
     return r;
   }
+  // grid capped at one resident wave of blocks (OCFFM_MISC_FILL: the side
+  // gradient, update and column-Gram step passes; no LDS)
+  bool misc_fill_ = !std::getenv("OCFFM_MISC_FILL") || std::atoi(std::getenv("OCFFM_MISC_FILL")) != 0;
+  template <typename... KArgs> unsigned mfill(void (*k)(KArgs...), unsigned grid) {
+    return misc_fill_ ? std::min(grid, resident(k, 0)) : grid;
+  }
   template <typename... KArgs, typename... A>
   void launch(void (*k)(KArgs...), dim3 grid, dim3 block, size_t smem, A... a) {
     static_assert(sizeof...(KArgs) == sizeof...(A), "kernel argument count");
@@ -2030,7 +2036,7 @@ template <typename real> class Problem final : public ProblemBase {
         }
         const real *ysum = ysum_on_ ? (const real *)ysum_.p : nullptr;
         prof_launch("gd_side_row", bytes, [&] {
-          launch(k_gd_side_seg<real, KP>, grid_for(own.nseg, 4 * Gm::NSG), BLOCK, 0, own.nseg, own.segs.p, own.ycol.p,
+          launch(k_gd_side_seg<real, KP>, mfill(k_gd_side_seg<real, KP>, grid_for(own.nseg, 4 * Gm::NSG)), BLOCK, 0, own.nseg, own.segs.p, own.ycol.p,
                  own.yt.p, h.Q1, own.bias.p, other.bias.p, own.s.p, bsum_.p + (h.user ? 1 : 0), n1, w_, r_, h_.p,
                  (uint64_t)other.R, ysum);
         });
@@ -3158,14 +3164,14 @@ template <typename real> class Problem final : public ProblemBase {
         const Fin<real> fin = make_fin(h, it);
         if (!comm_.active() || repl(h)) {
           prof_launch("hv_cgram", (double)h.D * KP * KP * rs + (double)h.D * KP * rs * (it > 1 ? 9 : 4), [&] {
-            launch(k_hv_cgram<real, KP>, grid_for(h.D, 4 * Gm::NSG, 1024), BLOCK, 0, (uint64_t)h.D, gram_of(h), fin,
+            launch(k_hv_cgram<real, KP>, mfill(k_hv_cgram<real, KP>, grid_for(h.D, 4 * Gm::NSG, 1024)), BLOCK, 0, (uint64_t)h.D, gram_of(h), fin,
                    (const uint8_t *)nullptr);
           });
           return;
         }
         if (h.F->excl) {  // owned field: this rank's columns are whole here; the dot products meet (feature_pass)
           prof_launch("hv_cgram", (double)h.D * KP * KP * rs + (double)h.D * KP * rs * (it > 1 ? 9 : 4), [&] {
-            launch(k_hv_cgram<real, KP>, grid_for(h.D, 4 * Gm::NSG, 1024), BLOCK, 0, (uint64_t)h.D, gram_of(h), fin,
+            launch(k_hv_cgram<real, KP>, mfill(k_hv_cgram<real, KP>, grid_for(h.D, 4 * Gm::NSG, 1024)), BLOCK, 0, (uint64_t)h.D, gram_of(h), fin,
                    (const uint8_t *)h.F->own.p);
           });
           allreduce_dev_d(dots_.p, 3);
@@ -3173,7 +3179,7 @@ template <typename real> class Problem final : public ProblemBase {
           return;
         }
         prof_launch("hv_cgram", (double)h.D * KP * KP * rs + (double)h.D * KP * rs * 4, [&] {
-          launch(k_hv_cgram<real, KP, 2>, grid_for(h.D, 4 * Gm::NSG, 1024), BLOCK, 0, (uint64_t)h.D, gram_of(h), fin,
+          launch(k_hv_cgram<real, KP, 2>, mfill(k_hv_cgram<real, KP, 2>, grid_for(h.D, 4 * Gm::NSG, 1024)), BLOCK, 0, (uint64_t)h.D, gram_of(h), fin,
                  (const uint8_t *)nullptr);
         });
         allreduce_dev(acc_.p, h.D * kp_);
@@ -3393,7 +3399,7 @@ template <typename real> class Problem final : public ProblemBase {
           // block-excluded base: the base does not depend on P1, no positive pass
           prof_launch("update_cross_rows", (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
                                                (double)own.R * KP * rs * 2, [&] {
-            launch(k_update_cross_rows<real, KP>, grid_for(own.R, 4 * Gm::NSG), BLOCK, 0, own.R, F.xptr.p, F.xidx.p,
+            launch(k_update_cross_rows<real, KP>, mfill(k_update_cross_rows<real, KP>, grid_for(own.R, 4 * Gm::NSG)), BLOCK, 0, own.R, F.xptr.p, F.xidx.p,
                    F.xval.p, (const real *)S_.p, h.P1, (real *)nullptr, F.one, Wf, (const real *)Vd_.p,
                    (const CgState *)st_.p, skip);
           });
@@ -3403,7 +3409,7 @@ template <typename real> class Problem final : public ProblemBase {
                              (double)own.R * KP * rs * 2 + (double)own.npos * (4 + 2 * rs) +
                              (double)other.R * KP * rs;
         prof_launch("update_cross_row", bytes, [&] {
-          launch(k_update_cross_seg<real, KP>, grid_for(own.nseg, 4 * Gm::NSG), BLOCK, 0,
+          launch(k_update_cross_seg<real, KP>, mfill(k_update_cross_seg<real, KP>, grid_for(own.nseg, 4 * Gm::NSG)), BLOCK, 0,
               own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, own.ycol.p, own.yt.p, h.Q1,
               (uint64_t)other.R, F.segd.p, F.segx.p, Wf,
               (const real *)Vd_.p, (const CgState *)st_.p, (const real *)nullptr, (const real *)nullptr,
@@ -3415,7 +3421,7 @@ template <typename real> class Problem final : public ProblemBase {
         const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
                              (double)own.R * KP * rs * 3 + (double)own.R * rs * 2 + (double)own.npos * (4 + 4 * rs);
         prof_launch("update_side_row", bytes, [&] {
-          launch(k_update_side_row<real, KP>, grid_for(own.R, 4 * Gm::NSG), BLOCK, 0,
+          launch(k_update_side_row<real, KP>, mfill(k_update_side_row<real, KP>, grid_for(own.R, 4 * Gm::NSG)), BLOCK, 0,
               own.R, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, h.Q1, own.bias.p, F.one, Wf,
               (const real *)Vd_.p, (const CgState *)st_.p, bsum_.p + (h.user ? 0 : 1), part_.p, tick_.p, skip);
         });

@@ -3239,7 +3239,7 @@ template <typename real> class Problem final : public ProblemBase {
           auto go = [&](auto fz, auto sc) {
             constexpr bool FZ = decltype(fz)::value, SC = decltype(sc)::value;
             unsigned grid = grid_for(own.R, 4 * Gm::NSG, FZ ? 2048u : 4096u);
-            if (row_fill_) grid = std::min(grid, resident(k_hs_side_row<real, KP, FZ, SC>, 0));
+            if (side_fill_) grid = std::min(grid, resident(k_hs_side_row<real, KP, FZ, SC>, 0));
             launch(k_hs_side_row<real, KP, FZ, SC>, grid, BLOCK, 0,
                 own.R, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, hess_cnt(h), h.Q1, w_, n1, h_.p, run, Rv_.p, Hv_.p, st_.p, it,
                 F.one, fin);
@@ -3575,6 +3575,8 @@ template <typename real> class Problem final : public ProblemBase {
   // hs_cross measured 1.6 % slower at its resident wave than at the cap
   bool row_fill_ = std::getenv("OCFFM_ROW_FILL") ? std::atoi(std::getenv("OCFFM_ROW_FILL")) != 0
                                                  : std::is_same<real, float>::value;
+  // the side rows (k_hs_side_row): both precisions (fp64 kkbox -0.3 %)
+  bool side_fill_ = !std::getenv("OCFFM_SIDE_FILL") || std::atoi(std::getenv("OCFFM_SIDE_FILL")) != 0;
   bool want_g_ = false;  // grad(): the gradient finalisation also stores G
   const real *qtq_ = nullptr;  // this cross half's Q^T Q: a slot of M_
   DevBuf<unsigned> tick_;

@@ -786,11 +786,29 @@ template <typename real> class Problem final : public ProblemBase {
     for (uint64_t n = 1;; n++) {
       const int v = __atomic_load_n(&run_host_[q], __ATOMIC_ACQUIRE);
       if (v) return v;
+      if (n % 4096 == 0 && __atomic_load_n(&run_host_[MAXCG + 3], __ATOMIC_ACQUIRE)) {
+        // the persistent CG kernel gave up on its grid barrier (not every
+        // block resident: another process on the GPU) and stops publishing
+        run_host_[MAXCG + 3] = 0;
+        throw Error(OCFFM_E_HIP, "persistent CG grid did not complete (k_cg_cgram spin limit)");
+      }
       if (n % 4096 == 0) {
         const hipError_t e = hipStreamQuery(stream_);
         if (e == hipSuccess) {  // stream drained: the word must be there now
           const int w = __atomic_load_n(&run_host_[q], __ATOMIC_ACQUIRE);
           if (w) return w;
+          // a full synchronisation, then ~50 ms of polls before calling it lost
+          HIPCHK(hipStreamSynchronize(stream_));
+          if (__atomic_load_n(&run_host_[MAXCG + 3], __ATOMIC_ACQUIRE)) {
+            run_host_[MAXCG + 3] = 0;
+            throw Error(OCFFM_E_HIP, "persistent CG grid did not complete (k_cg_cgram spin limit)");
+          }
+          const auto t0 = std::chrono::steady_clock::now();
+          do {
+            const int x = __atomic_load_n(&run_host_[q], __ATOMIC_ACQUIRE);
+            if (x) return x;
+            __builtin_ia32_pause();
+          } while (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(50));
           throw Error(OCFFM_E_STATE, "CG verdict " + std::to_string(q) + " never published");
         }
         if (e != hipErrorNotReady) HIPCHK(e);

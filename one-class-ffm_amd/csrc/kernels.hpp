@@ -60,6 +60,9 @@ template <typename real, int KP> struct Geo {
 constexpr int BLOCK = 256;   // 4 waves
 // Minimum waves per SIMD the positive-gather row passes are compiled for
 // (1 = the compiler's choice); experiment builds set them with -D.
+#ifndef OCFFM_HS_OCC64
+#define OCFFM_HS_OCC64 1  // the fp64 build of k_hs_cross_seg (experiment builds: -D)
+#endif
 #ifndef OCFFM_HS_OCC
 #define OCFFM_HS_OCC 1
 #endif
@@ -2179,7 +2182,7 @@ __global__ __launch_bounds__(BLOCK) void k_cg_cgram(uint64_t D, const real *__re
 // tau = X_i (V QTQ) = phi_i QTQ).  QTQ staged in LDS; phi_i's components
 // are broadcast by DPP for the k x k product (sg_vecmat).
 template <typename real, int KP, bool MLDS, int PW_ = 32>
-__global__ __launch_bounds__(BLOCK, OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
+__global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_HS_OCC64 : OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                         const int64_t *__restrict__ xptr,
                                                         const uint32_t *__restrict__ xidx,
                                                         const real *__restrict__ xval, const real *__restrict__ V,

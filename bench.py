@@ -249,10 +249,6 @@ def main():
         # N ranks on one GPU (tests of this script's multi-rank flow on a
         # one-GPU box): the library's all-reduces go through gloo on the host
         local = 0
-        # no persistent CG kernel: its grid barrier needs every block of the
-        # grid resident at once, which N processes sharing one GPU cannot
-        # promise (one process per GPU, as in a real N-GPU run, can)
-        os.environ["OCFFM_CGP"] = "0"
 
         def allreduce(arr):
             dist.all_reduce(torch.from_numpy(arr))

@@ -224,6 +224,12 @@ int ocffm_problem_reset_stats(ocffm_problem *p);
 /* Algorithmic HBM bytes of the epochs run since the last reset
  * (SURVEY §8d formula with the actual CG counts). */
 int ocffm_problem_alg_bytes(ocffm_problem *p, double *bytes);
+/* Diagnostic event counters since create (no reference counterpart):
+ * "cgp_launches" (persistent column-Gram CG launches), "cgp_recovered"
+ * (launches whose grid gave up on its barrier and whose solve was finished
+ * per step), "cgp_refused" (cooperative launches the runtime refused).
+ * An unknown name reads 0. */
+int ocffm_problem_counter(ocffm_problem *p, const char *name, int64_t *value);
 int ocffm_problem_sync(ocffm_problem *p);
 /* Digests (FNV-1a over the bytes) of every array of the device data layout
  * the problem built from its ImpData (per-field CSR of split_fields,

@@ -2103,8 +2103,32 @@ __global__ __launch_bounds__(BLOCK) void k_pg_step(uint64_t D, uint32_t QB, cons
 // verdict (the same arithmetic as cg_publish, through agent-scope stores)
 // and then releases the grid through a generation word that the other
 // blocks poll (bounded spin); the next step reads the scalars with
-// agent-scope loads.  The grid must be co-resident (host: at most one
-// block per CU).  No host round trip or kernel boundary between steps.
+// agent-scope loads.  No host round trip or kernel boundary between steps.
+//
+// Co-residency (round 6).  The host launches the grid cooperatively (the
+// runtime refuses a grid that cannot be resident, and the host then takes
+// the two-launch path), but another process's kernels can still hold CUs
+// or the queue can be time-sliced, so the barrier is also made safe to give
+// up: the generation word is released and aborted by compare-and-swap.  A
+// waiter that spins past `spin_max` swaps the unreleased word for CGP_ABORT;
+// the last block of the step swaps in the release.  Exactly one of the two
+// wins.  Every block always finishes the step it is in and takes its
+// ticket (the tickets reset themselves), and the last block publishes the
+// step's scalars and verdict BEFORE its swap, so an abort at barrier `it`
+// leaves every column at step `it` with the scalars of step `it` in
+// CgState: exactly the state the two-launch path (k_hv_cgram) continues
+// from at step it+1.  The abort is reported as `it` in the host-mapped
+// word and as 1 in `abort_dev`, which guards the update kernels queued
+// behind this launch (they return at entry); the host then resets both
+// words and the generation word and finishes the solve per step.
+// stall_step (tests only): the grid's last block sleeps before the column
+// work of that step, long enough for the others to give up.
+constexpr unsigned CGP_ABORT = 0xffffffffu;
+__device__ __forceinline__ void cgp_report_abort(int *err_host, int *abort_dev, int it) {
+  __hip_atomic_store(abort_dev, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(err_host, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 __device__ __forceinline__ double ald(const double *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -2113,10 +2137,11 @@ __device__ __forceinline__ void ast(double *p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void ast(int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-constexpr unsigned CGP_SPIN_MAX = 1u << 24;  // ~seconds of s_sleep 1: a stuck grid gives up (err) instead of hanging
+constexpr unsigned CGP_SPIN_MAX = 1u << 22;  // ~0.1 s of s_sleep 1: then the grid gives up (recoverable)
 template <typename real, int KP>
 __global__ __launch_bounds__(BLOCK) void k_cg_cgram(uint64_t D, const real *__restrict__ G, Fin<real> f,
-                                                    unsigned *__restrict__ gen, unsigned gen0, int *__restrict__ err) {
+                                                    unsigned *__restrict__ gen, unsigned gen0, int *__restrict__ err_host,
+                                                    int *__restrict__ abort_dev, unsigned spin_max, int stall_step) {
   using Gm = Geo<real, KP>;
   WAVE_SETUP
   const int sg = lane / Gm::LPR, li = lane % Gm::LPR;
@@ -2127,6 +2152,8 @@ __global__ __launch_bounds__(BLOCK) void k_cg_cgram(uint64_t D, const real *__re
     const bool upd = it > 1;
     const real alpha = upd ? (real)ald(&st->alpha) : (real)0, beta = upd ? (real)ald(&st->beta) : (real)0;
     f.it = it;
+    if (it == stall_step && blockIdx.x == gridDim.x - 1 && gridDim.x > 1)
+      for (int q = 0; q < 4000; q++) __builtin_amdgcn_s_sleep(127);
     double dsum[3] = {0, 0, 0};
     for (uint64_t c = wave * Gm::NSG + sg; c < D; c += nwaves * Gm::NSG) {
       const FinOps<real> ops = fin_load<real, KP, 1>(f, (uint32_t)c, upd, li);
@@ -2154,18 +2181,48 @@ __global__ __launch_bounds__(BLOCK) void k_cg_cgram(uint64_t D, const real *__re
         if (f.run_host)
           __hip_atomic_store(f.run_host + it + 1, go ? RUN_GO : RUN_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store above (and the tickets' reset) landed
-        __hip_atomic_store(gen, gen0 + (unsigned)it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // release by swap: fails only if a waiter already gave up on this
+        // barrier.  The fence makes any plain store of this block visible to
+        // the other XCDs before the release (today every value crossing
+        // blocks is itself an agent-scope atomic; the fence keeps that from
+        // being a requirement).
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        unsigned cur = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int ok = 0;
+        while (cur != CGP_ABORT) {
+          if (__hip_atomic_compare_exchange_strong(gen, &cur, gen0 + (unsigned)it, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)) {
+            ok = 1;
+            break;
+          }
+        }
+        if (!ok) cgp_report_abort(err_host, abort_dev, it);
+        s_ok = ok;
       }
       __syncthreads();
+      if (!s_ok) return;
     } else {
       if (threadIdx.x == 0) {
         int ok = 1;
         unsigned spins = 0;
-        while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen0 + (unsigned)it) {
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > CGP_SPIN_MAX) {
+        for (;;) {
+          // relaxed polls (an acquire per poll would invalidate this XCD's L2
+          // every time), one acquire fence once released
+          unsigned cur = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (cur == gen0 + (unsigned)it) {  // released
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            break;
+          }
+          if (cur == CGP_ABORT) {                 // another waiter gave up
             ok = 0;
-            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > spin_max &&
+              __hip_atomic_compare_exchange_strong(gen, &cur, CGP_ABORT, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)) {
+            cgp_report_abort(err_host, abort_dev, it);
+            ok = 0;
             break;
           }
         }

@@ -356,6 +356,7 @@ struct ProblemBase {
   bool profiling = false;
   std::string prof_filter;
   double alg_bytes = 0;
+  std::map<std::string, int64_t> counters;  // diagnostics (ocffm_problem_counter)
 };
 
 struct Comm {
@@ -466,6 +467,13 @@ template <typename real> class Problem final : public ProblemBase {
       ncu_ = (unsigned)std::max(1, ncu);
     }
     cgp_gen_buf_.alloc(1);
+    cgp_abort_.alloc(1);
+    {
+      int dev = 0, coop = 0;
+      HIPCHK(hipGetDevice(&dev));
+      if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess) coop = 0;
+      cgp_coop_ = cgp_coop_ && coop != 0;
+    }
     std::memset(run_host_, 0, sizeof(int) * (MAXCG + 2));
     HIPCHK(hipHostGetDevicePointer((void **)&run_host_dev_, run_host_, 0));
     if (comm_.host_fn) HIPCHK(hipHostMalloc((void **)&stage_, Dmax * kp_ * sizeof(real), hipHostMallocDefault));
@@ -782,16 +790,14 @@ template <typename real> class Problem final : public ProblemBase {
   // Spin on the host-mapped verdict of CG iteration q until a finalising
   // kernel has published it.  Every few thousand polls the stream is
   // queried, so a faulted kernel surfaces as an error instead of a hang.
+  // CGP_GAVE_UP: the persistent CG grid gave up on its barrier (the word
+  // MAXCG + 3 holds the step it completed; the caller recovers, `half`).
+  static constexpr int CGP_GAVE_UP = -1;
   int poll_verdict(int q) {
     for (uint64_t n = 1;; n++) {
       const int v = __atomic_load_n(&run_host_[q], __ATOMIC_ACQUIRE);
       if (v) return v;
-      if (n % 4096 == 0 && __atomic_load_n(&run_host_[MAXCG + 3], __ATOMIC_ACQUIRE)) {
-        // the persistent CG kernel gave up on its grid barrier (not every
-        // block resident: another process on the GPU) and stops publishing
-        run_host_[MAXCG + 3] = 0;
-        throw Error(OCFFM_E_HIP, "persistent CG grid did not complete (k_cg_cgram spin limit)");
-      }
+      if (n % 4096 == 0 && __atomic_load_n(&run_host_[MAXCG + 3], __ATOMIC_ACQUIRE)) return CGP_GAVE_UP;
       if (n % 4096 == 0) {
         const hipError_t e = hipStreamQuery(stream_);
         if (e == hipSuccess) {  // stream drained: the word must be there now
@@ -799,10 +805,7 @@ template <typename real> class Problem final : public ProblemBase {
           if (w) return w;
           // a full synchronisation, then ~50 ms of polls before calling it lost
           HIPCHK(hipStreamSynchronize(stream_));
-          if (__atomic_load_n(&run_host_[MAXCG + 3], __ATOMIC_ACQUIRE)) {
-            run_host_[MAXCG + 3] = 0;
-            throw Error(OCFFM_E_HIP, "persistent CG grid did not complete (k_cg_cgram spin limit)");
-          }
+          if (__atomic_load_n(&run_host_[MAXCG + 3], __ATOMIC_ACQUIRE)) return CGP_GAVE_UP;
           const auto t0 = std::chrono::steady_clock::now();
           do {
             const int x = __atomic_load_n(&run_host_[q], __ATOMIC_ACQUIRE);
@@ -3109,20 +3112,76 @@ template <typename real> class Problem final : public ProblemBase {
   double cgp_step_bytes(const HalfCtx &h) const {
     return (double)h.D * kp_ * kp_ * sizeof(real) + (double)h.D * kp_ * sizeof(real) * 9;
   }
-  void cg_persist(HalfCtx &h) {
+  // Returns false if nothing was launched (a cooperative launch the runtime
+  // refused: the caller takes the two-launch path for the whole half).
+  bool cg_persist(HalfCtx &h) {
+    bool ok = true;
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
       using Gm = Geo<real, KP>;
-      const Fin<real> fin = make_fin(h, 1);
-      // co-resident grid: at most one block per CU
+      Fin<real> fin = make_fin(h, 1);
+      // at most one block per CU (co-resident unless other work holds the CUs)
       const unsigned grid = (unsigned)std::min<uint64_t>((h.D + 4 * Gm::NSG - 1) / (4 * Gm::NSG), ncu_);
-      const unsigned g0 = cgp_gen_;
+      if (cgp_gen_ > 0xf0000000u) {  // keep clear of CGP_ABORT
+        HIPCHK(hipMemsetAsync(cgp_gen_buf_.p, 0, sizeof(unsigned), stream_));
+        cgp_gen_ = 1;
+      }
+      unsigned g0 = cgp_gen_;
       cgp_gen_ += MAXCG + 1;
+      const real *G = gram_of(h);
+      uint64_t D = h.D;
+      unsigned *genp = cgp_gen_buf_.p;
+      int *errh = run_host_dev_ + MAXCG + 3, *abd = cgp_abort_.p;
+      unsigned spin = cgp_spin_;
+      int stall = cgp_stall_;
+      counters["cgp_launches"]++;
       prof_launch("cg_cgram", 0.0, [&] {
-        launch(k_cg_cgram<real, KP>, grid, BLOCK, 0, (uint64_t)h.D, gram_of(h), fin, cgp_gen_buf_.p, g0,
-               run_host_dev_ + MAXCG + 3);
+        if (!cgp_coop_) {
+          launch(k_cg_cgram<real, KP>, grid, BLOCK, 0, D, G, fin, genp, g0, errh, abd, spin, stall);
+          return;
+        }
+        // cooperative: the runtime checks that the grid can be resident at
+        // once and refuses it otherwise (then: the per-step path)
+        void *args[] = {&D, (void *)&G, &fin, &genp, &g0, &errh, &abd, &spin, &stall};
+        if (arm_first_) HIPCHK(hipEventRecord(arm_a_, stream_));
+        const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(k_cg_cgram<real, KP>), dim3(grid),
+                                                        dim3(BLOCK), args, 0u, stream_);
+        if (e == hipErrorCooperativeLaunchTooLarge) {
+          (void)hipGetLastError();
+          counters["cgp_refused"]++;
+          ok = false;
+        } else {
+          HIPCHK(e);
+        }
+        if (arm_first_) {
+          HIPCHK(hipEventRecord(arm_b_, stream_));
+          arm_first_ = false;
+        }
       });
     });
+    return ok;
+  }
+  // The persistent grid gave up on a barrier (kernels.hpp k_cg_cgram): every
+  // column is at step `ab` (the value in the host word) with that step's
+  // scalars and verdict published, and the update queued behind the launch
+  // returned at entry.  Reset the abort words and the generation word, read
+  // the verdicts up to ab + 1, and return the step the per-step loop
+  // continues with.
+  template <class Ex> int cgp_recover(Ex &examine, bool &gave_up, bool &queued) {
+    HIPCHK(hipStreamSynchronize(stream_));
+    const int ab = __atomic_load_n(&run_host_[MAXCG + 3], __ATOMIC_ACQUIRE);
+    if (ab < 1 || ab > MAXCG) throw Error(OCFFM_E_STATE, "persistent CG: bad abort step " + std::to_string(ab));
+    run_host_[MAXCG + 3] = 0;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    HIPCHK(hipMemsetAsync(cgp_abort_.p, 0, sizeof(int), stream_));
+    HIPCHK(hipMemsetAsync(cgp_gen_buf_.p, 0, sizeof(unsigned), stream_));
+    cgp_gen_ = 1;
+    counters["cgp_recovered"]++;
+    gave_up = false;
+    queued = false;
+    examine(ab + 1);
+    if (gave_up) throw Error(OCFFM_E_STATE, "persistent CG: verdict missing after recovery");
+    return ab + 1;
   }
 
   // Processing order of a side's segments for the cross row passes
@@ -3295,10 +3354,14 @@ template <typename real> class Problem final : public ProblemBase {
     // an event recorded between two CG steps cost ~5 us of GPU idle per step
     // (measured: 6.7 us vs 1.1 us at the boundaries without one).
     int nr = 0, known = 0;
-    bool done = false;
+    bool done = false, gave_up = false;
     auto examine = [&](int upto) {
       for (int q = known + 1; q <= upto && q <= MAXCG && !done; q++) {
         const int v = host_wait([&] { return poll_verdict(q); });
+        if (v == CGP_GAVE_UP) {
+          gave_up = true;
+          return;
+        }
         if (v != RUN_GO) done = true;
         else nr = q;
         known = q;
@@ -3328,25 +3391,27 @@ template <typename real> class Problem final : public ProblemBase {
     col_grams(h);
     hot_grams(h);
     if (io) io_begin(h);
+    int it0 = 1;
     if (cgp_ok(h)) {
       // the whole CG in one persistent launch, the update queued right
-      // behind it (no speculation, no host round trip inside the half)
+      // behind it (no speculation, no host round trip inside the half); the
+      // update returns at entry if the grid gave up on its barrier
       prof_tag_ = 1;
-      cg_persist(h);
+      const bool launched = cg_persist(h);
       prof_tag_ = 0;
-      finish_half(h, nullptr);
-      queued = true;
-      examine(MAXCG);
-      if (run_host_[MAXCG + 3]) {
-        run_host_[MAXCG + 3] = 0;
-        throw Error(OCFFM_E_HIP, "persistent CG grid did not complete (k_cg_cgram spin limit)");
-      }
-      if (profiling && pending_.size() > pend0) {  // its bytes: the steps that ran
-        for (size_t q = pend0; q < pending_.size(); q++)
-          if (pending_[q].name == "cg_cgram") pending_[q].bytes = (double)nr * cgp_step_bytes(h);
+      if (launched) {
+        finish_half(h, cgp_abort_.p);
+        queued = true;
+        examine(MAXCG);
+        if (gave_up) it0 = cgp_recover(examine, gave_up, queued);
+        if (profiling && pending_.size() > pend0) {  // its bytes: the steps that ran in it
+          for (size_t q = pend0; q < pending_.size(); q++)
+            if (pending_[q].name == "cg_cgram")
+              pending_[q].bytes = (double)(it0 > 1 ? it0 - 1 : nr) * cgp_step_bytes(h);
+        }
       }
     }
-    for (int it = 1; it <= MAXCG && !done && !queued; it++) {
+    for (int it = it0; it <= MAXCG && !done && !queued; it++) {
       prof_tag_ = it;
       hv_pass(h, it);
       prof_tag_ = 0;
@@ -3609,8 +3674,14 @@ template <typename real> class Problem final : public ProblemBase {
   // persistent column-Gram CG (k_cg_cgram, OCFFM_CGP): the grid's release
   // word (monotonic across launches), the CU count that bounds its grid
   DevBuf<unsigned> cgp_gen_buf_;
-  unsigned cgp_gen_ = 0, ncu_ = 256;
+  DevBuf<int> cgp_abort_;  // 1: the last persistent grid gave up (guards its queued update)
+  unsigned cgp_gen_ = 1, ncu_ = 256;
   bool cgp_on_ = !std::getenv("OCFFM_CGP") || std::atoi(std::getenv("OCFFM_CGP")) != 0;
+  // OCFFM_CGP_COOP=0: plain launch instead of the cooperative one
+  bool cgp_coop_ = !std::getenv("OCFFM_CGP_COOP") || std::atoi(std::getenv("OCFFM_CGP_COOP")) != 0;
+  // tests: a short spin limit and one block stalled at a given step force the give-up
+  unsigned cgp_spin_ = std::getenv("OCFFM_CGP_SPIN") ? (unsigned)std::atol(std::getenv("OCFFM_CGP_SPIN")) : CGP_SPIN_MAX;
+  int cgp_stall_ = std::getenv("OCFFM_CGP_STALL") ? std::atoi(std::getenv("OCFFM_CGP_STALL")) : 0;
   real *stage_ = nullptr;
   static constexpr uint64_t DSTAGE = 64;
   double *dstage_ = nullptr;  // host all-reduce stage of the owned-field dot products
@@ -3946,6 +4017,13 @@ int ocffm_problem_reset_stats(ocffm_problem *prob) {
   });
 }
 int ocffm_problem_alg_bytes(ocffm_problem *prob, double *bytes) { PROB_CALL(*bytes = prob->p->alg_bytes); }
+int ocffm_problem_counter(ocffm_problem *prob, const char *name, int64_t *value) {
+  PROB_CALL({
+    if (!name || !value) throw Error(OCFFM_E_ARG, "null argument");
+    const auto it = prob->p->counters.find(name);
+    *value = it == prob->p->counters.end() ? 0 : it->second;
+  });
+}
 int ocffm_problem_sync(ocffm_problem *prob) { PROB_CALL(prob->p->sync()); }
 int ocffm_problem_layout_digest(ocffm_problem *prob, char *names, uint64_t *digests, int cap, int *count) {
   return guarded([&] {

@@ -67,7 +67,7 @@ EXPORTS = [
     "ocffm_problem_validate_forced", "ocffm_problem_test_rows", "ocffm_problem_save_binary", "ocffm_problem_load_binary",
     "ocffm_problem_cg_log", "ocffm_problem_set_profiling", "ocffm_problem_set_profile_filter",
     "ocffm_problem_kernel_stats",
-    "ocffm_problem_reset_stats", "ocffm_problem_alg_bytes", "ocffm_problem_sync",
+    "ocffm_problem_reset_stats", "ocffm_problem_alg_bytes", "ocffm_problem_counter", "ocffm_problem_sync",
     "ocffm_problem_layout_digest", "ocffm_problem_destroy",
     "ocffm_sgd_param_default", "ocffm_sgd_create", "ocffm_sgd_create_dist", "ocffm_sgd_create_dist_host", "ocffm_sgd_epoch",
     "ocffm_sgd_average", "ocffm_sgd_phi", "ocffm_sgd_get", "ocffm_sgd_set_w", "ocffm_sgd_get_info",
@@ -122,6 +122,7 @@ def lib():
     L.ocffm_problem_set_profile_filter.argtypes = [vp, C.c_char_p]
     L.ocffm_problem_kernel_stats.argtypes = [vp, C.POINTER(_KStat), i32, C.POINTER(C.c_int)]
     L.ocffm_problem_alg_bytes.argtypes = [vp, C.POINTER(dbl)]
+    L.ocffm_problem_counter.argtypes = [vp, C.c_char_p, C.POINTER(C.c_int64)]
     L.ocffm_problem_layout_digest.argtypes = [vp, vp, vp, i32, C.POINTER(C.c_int)]
     L.ocffm_problem_destroy.argtypes = [vp]
     L.ocffm_problem_destroy.restype = None
@@ -491,6 +492,12 @@ class ImpProblem:
         b = C.c_double(0)
         _check(lib().ocffm_problem_alg_bytes(self.h, C.byref(b)))
         return b.value
+
+    def counter(self, name: str) -> int:
+        """Diagnostic event counter (include/ocffm.h ocffm_problem_counter)."""
+        v = C.c_int64(0)
+        _check(lib().ocffm_problem_counter(self.h, name.encode(), C.byref(v)))
+        return v.value
 
     def sync(self) -> None:
         _check(lib().ocffm_problem_sync(self.h))

@@ -188,16 +188,14 @@ def _dist_dataset(name):
     return synth.kkbox(seed=5, m=300, n=400, mean=12.0, name="kkbox_dist")
 
 
-# Several ranks share the one GPU in these tests: the persistent CG kernel's
-# grid barrier needs all of its blocks resident at once, which other ranks'
-# kernels on the same GPU can prevent (one process per GPU, as in a real
-# multi-GPU run, cannot), so the workers run the CG steps as separate
-# launches (the persistent kernel is parity-tested on one rank).
-NO_CGP = dict(OCFFM_CGP="0")
+# Several ranks share the one GPU in these tests, so the persistent CG
+# kernel's grid (k_cg_cgram, on the replicated halves) can find CUs held by
+# other ranks' kernels: it then gives up on its barrier and the solve is
+# finished per step (solver.hip cgp_recover), which these runs exercise.
 
 
 def _gpu_worker(rank, port, out_dir, world, name="tiny"):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **NO_CGP)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import ocffm
 
@@ -360,7 +358,7 @@ def test_rccl_one_rank_matches_single():
 
 
 def _fp32_worker(rank, port, out_dir, world):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **NO_CGP)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import ocffm
 

@@ -56,6 +56,9 @@ SETS = {
                                     nnz_user=1, mean_pos=12.0, vals="real"), dict()),
     "outbrain": (lambda: synth.general(seed=32, m=400, n=60, fu=2, fv=2, k=64, mean_pos=1.0, test_rows=40,
                                        name="outbrain"), dict(k=64)),
+    # the headline configuration at its own size (30,755 x 100,000, k = 32,
+    # 2.1 M positives; tests/test_gpu_parity.py test_kkbox_full_size_parity_fp64)
+    "kkbox_full": (lambda: synth.kkbox(test_frac=0.05), dict()),
 }
 
 
@@ -101,8 +104,11 @@ def run_gpu(ds, kw, E, exact):
 
 def envelope(E, path, only=None):
     res = {}
+    E_file = E
     if only and os.path.exists(path):  # add / refresh some sets of an existing envelope
-        res = json.load(open(path))["sets"]
+        prev = json.load(open(path))
+        res = prev["sets"]
+        E_file = max(E, prev.get("epochs", E))
     for name, (mk, kw) in SETS.items():
         if only and name not in only:
             continue
@@ -117,7 +123,7 @@ def envelope(E, path, only=None):
         res[name] = env
         print(f"{name:11s} " + " ".join(f"{x:.2e}" for x in env), flush=True)
     with open(path, "w") as f:
-        json.dump({"epochs": E, "threads": [2, 3, 4, 6, 8, 16], "repeats": 2,
+        json.dump({"epochs": E_file, "threads": [2, 3, 4, 6, 8, 16], "repeats": 2,
                    "what": "max relative difference (W, H, P, Q, a, b, y~) of the oracle at T threads vs 1 thread, per epoch",
                    "sets": res}, f, indent=1)
 

@@ -2105,11 +2105,14 @@ __global__ __launch_bounds__(BLOCK) void k_pg_step(uint64_t D, uint32_t QB, cons
 // blocks poll (bounded spin); the next step reads the scalars with
 // agent-scope loads.  No host round trip or kernel boundary between steps.
 //
-// Co-residency (round 6).  The host launches the grid cooperatively (the
-// runtime refuses a grid that cannot be resident, and the host then takes
-// the two-launch path), but another process's kernels can still hold CUs
-// or the queue can be time-sliced, so the barrier is also made safe to give
-// up: the generation word is released and aborted by compare-and-swap.  A
+// Co-residency (round 6).  The host checks the grid against the occupancy
+// API (at most one block per CU) and can launch it cooperatively
+// (OCFFM_CGP_COOP=1: the runtime's own check, measured +0.27 ms per kkbox
+// epoch of host launch cost, nothing more: a plain launch of the same grid
+// has the same residency).  Neither stops another process's kernels from
+// holding CUs or the queue from being time-sliced, so the barrier is made
+// safe to give up: the generation word is released and aborted by
+// compare-and-swap.  A
 // waiter that spins past `spin_max` swaps the unreleased word for CGP_ABORT;
 // the last block of the step swaps in the release.  Exactly one of the two
 // wins.  Every block always finishes the step it is in and takes its
@@ -2124,6 +2127,20 @@ __global__ __launch_bounds__(BLOCK) void k_pg_step(uint64_t D, uint32_t QB, cons
 // stall_step (tests only): the grid's last block sleeps before the column
 // work of that step, long enough for the others to give up.
 constexpr unsigned CGP_ABORT = 0xffffffffu;
+// Memory ordering.  Everything that crosses blocks inside the launch is an
+// agent-scope (sc1) atomic on both sides — the partial dot products and
+// tickets (last_block), the CG scalars and verdicts (ast / ald), the
+// generation word — and every storing wave drains vmcnt before its ticket
+// or the release (MI355X guide, Consumer bullet conditions 1-4); the CG
+// vectors are only ever touched by the block that owns the column.  So no
+// L2 write-back / invalidate is needed at the barrier.  -DOCFFM_CGP_FENCE=1
+// adds an agent release fence before the release and an acquire fence
+// after it (for plain stores read across blocks, should any be added):
+// measured +0.07 ms per kkbox epoch (a write-back of the XCD's dirty L2 per
+// step).
+#ifndef OCFFM_CGP_FENCE
+#define OCFFM_CGP_FENCE 0
+#endif
 __device__ __forceinline__ void cgp_report_abort(int *err_host, int *abort_dev, int it) {
   __hip_atomic_store(abort_dev, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(err_host, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2182,11 +2199,8 @@ __global__ __launch_bounds__(BLOCK) void k_cg_cgram(uint64_t D, const real *__re
           __hip_atomic_store(f.run_host + it + 1, go ? RUN_GO : RUN_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store above (and the tickets' reset) landed
         // release by swap: fails only if a waiter already gave up on this
-        // barrier.  The fence makes any plain store of this block visible to
-        // the other XCDs before the release (today every value crossing
-        // blocks is itself an agent-scope atomic; the fence keeps that from
-        // being a requirement).
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        // barrier (fence: see OCFFM_CGP_FENCE above)
+        if constexpr (OCFFM_CGP_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         unsigned cur = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int ok = 0;
         while (cur != CGP_ABORT) {
@@ -2206,11 +2220,11 @@ __global__ __launch_bounds__(BLOCK) void k_cg_cgram(uint64_t D, const real *__re
         int ok = 1;
         unsigned spins = 0;
         for (;;) {
-          // relaxed polls (an acquire per poll would invalidate this XCD's L2
-          // every time), one acquire fence once released
+          // relaxed sc1 polls (an acquire per poll would invalidate this
+          // CU's L1 every time)
           unsigned cur = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (cur == gen0 + (unsigned)it) {  // released
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            if constexpr (OCFFM_CGP_FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             break;
           }
           if (cur == CGP_ABORT) {                 // another waiter gave up
@@ -2238,7 +2252,27 @@ __global__ __launch_bounds__(BLOCK) void k_cg_cgram(uint64_t D, const real *__re
 // + [first] w phi_i QTQ, phi_i = X_i p  (hs_cross row body, ffm.cpp:715-738;
 // tau = X_i (V QTQ) = phi_i QTQ).  QTQ staged in LDS; phi_i's components
 // are broadcast by DPP for the k x k product (sg_vecmat).
-template <typename real, int KP, bool MLDS, int PW_ = 32>
+//
+// TT (round 6; fp32, KP 16 / 32 / 64, rows with several nodes — one-node
+// fields take tau per column in the feature pass instead): tau on the matrix
+// cores.  The block walks SB = 4 NSG consecutive segments per iteration;
+// each subgroup puts its phi (first segments; else zero) in an LDS tile and
+// does its gathers, then the block's [phi rows] x QTQ product is cut into
+// 16 x 16 tiles, one per wave, each a chain of KP / 4 v_mfma_f32_16x16x4f32
+// (TMma's K order: A one 16-B LDS read of a phi row, B one 16-B read of QTQ
+// staged as TMma::stage does), the tau tile goes back to LDS and each
+// subgroup adds its row.  sg_vecmat had read QTQ once per row: KP 16-B LDS
+// reads per lane and row (at k = 64 ~30 % of outbrain's user-half pass).
+template <typename real, int KP> struct TauTile {
+  using G = Geo<real, KP>;
+  static constexpr bool OK = TMma<real, KP>::OK && std::is_same<real, float>::value;
+  static constexpr int SB = 4 * G::NSG;                      // segments per block iteration
+  static constexpr int TR = SB / 16, TC = KP / 16;           // 16 x 16 output tiles
+  static constexpr int LD = KP + 4;                          // padded row stride (floats) of the phi / tau tiles
+  static constexpr size_t bytes() { return (size_t)KP * KP * 4 + 2 * (size_t)SB * LD * 4; }
+  static_assert(!OK || TR * TC <= 4 * ((TR * TC + 3) / 4), "tiles");
+};
+template <typename real, int KP, bool MLDS, int PW_ = 32, bool TT = false>
 __global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_HS_OCC64 : OCFFM_HS_OCC) void k_hs_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                         const int64_t *__restrict__ xptr,
                                                         const uint32_t *__restrict__ xidx,
@@ -2265,7 +2299,10 @@ __global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_HS_OCC64 : OCFFM_H
   extern __shared__ __align__(16) unsigned char smem_raw[];
   real *Qs = reinterpret_cast<real *>(smem_raw);
   const real *Qp = QTQ;
-  if (MLDS) {  // QTQ null: the tau term is added per column by the feature pass (k_feat TAU)
+  if constexpr (TT) {
+    TMma<real, KP>::stage(QTQ, 1, Qs);  // B operand layout (tau tiles)
+    __syncthreads();
+  } else if (MLDS) {  // QTQ null: the tau term is added per column by the feature pass (k_feat TAU)
     if (QTQ)
       for (int t = threadIdx.x; t < KP * KP; t += BLOCK) Qs[t] = QTQ[t];
     __syncthreads();
@@ -2277,7 +2314,7 @@ __global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_HS_OCC64 : OCFFM_H
   // Per segment: phi from the row's node(s), the partner-row gathers, tau.
   // A hot row (hs != HOT_NONE) reads its Gram instead: its first segment
   // stores (1 - w) G_i phi_i (+ tau), its other segments zero.
-  auto seg_out = [&](const Seg &sgm, uint32_t d1, real x1, uint32_t hs) -> vec_t<real> {
+  auto seg_out = [&](const Seg &sgm, uint32_t d1, real x1, uint32_t hs, vec_t<real> *phi_out) -> vec_t<real> {
     const uint64_t i = sgm.row;
     if (hs != HOT_NONE && !seg_first(sgm)) return vzero<real>();
     uint32_t jj[PP::UT];  // the first pass's columns go out with the phi gather
@@ -2313,11 +2350,51 @@ __global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_HS_OCC64 : OCFFM_H
       });
     }
     vec_t<real> out = vsplat<real>(cpos) * ka;
-    if (QTQ && seg_first(sgm)) {
+    if constexpr (TT) {
+      if (seg_first(sgm)) *phi_out = phi;  // tau: the block's MFMA tile
+    } else if (QTQ && seg_first(sgm)) {
       out += vsplat<real>((real)w) * sg_vecmat<real, KP>(phi, Qp, li);
     }
     return out;
   };
+  if constexpr (TT) {
+    using TTl = TauTile<real, KP>;
+    constexpr int SB = TTl::SB, LD = TTl::LD;
+    real *Ph = Qs + KP * KP, *Tl = Ph + SB * LD;
+    const int wv = threadIdx.x >> 6, rowl = wv * G::NSG + sg;  // this subgroup's tile row
+    for (uint64_t base = (uint64_t)blockIdx.x * SB; base < nseg; base += (uint64_t)gridDim.x * SB) {
+      const uint64_t sx = base + rowl;
+      vec_t<real> phi = vzero<real>(), out = vzero<real>();
+      bool first = false;
+      if (sx < nseg) {
+        const Seg sgm = segs[sx];
+        first = seg_first(sgm);
+        out = seg_out(sgm, segd ? segd[sx] : 0u, segd ? segx[sx] : (real)0, HOT_NONE, &phi);
+      }
+      *reinterpret_cast<vec_t<real> *>(Ph + rowl * LD + li * G::VE) = phi;
+      __syncthreads();
+      // wave wv: output tiles wv, wv + 4, ... of the TR x TC grid
+      for (int t = wv; t < TTl::TR * TTl::TC; t += 4) {
+        const int tr = t % TTl::TR, tc = t / TTl::TR, m = lane & 15, q = lane >> 4;
+        f4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < KP / 16; j++) {
+          const f4v a = *reinterpret_cast<const f4v *>(Ph + (tr * 16 + m) * LD + 16 * j + 4 * q);
+          const f4v b = *reinterpret_cast<const f4v *>(Qs + ((4 * j + q) * KP + tc * 16 + m) * 4);
+#pragma unroll
+          for (int u = 0; u < 4; u++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) Tl[(tr * 16 + 4 * q + r) * LD + tc * 16 + m] = acc[r];
+      }
+      __syncthreads();
+      if (sx < nseg) {
+        if (first) out += vsplat<real>((real)w) * *reinterpret_cast<const vec_t<real> *>(Tl + rowl * LD + li * G::VE);
+        vst<real>(h + sx * KP + li * G::VE, out);
+      }
+    }
+    return;
+  }
   // Grid-stride over segments with the next segment's descriptor (and its
   // node) in flight while the current one is gathered.
   // sord (optional): the order in which the subgroups take the segments
@@ -2345,7 +2422,7 @@ __global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_HS_OCC64 : OCFFM_H
     const real x1 = nx;
     const uint64_t sx = nsx;
     if (s + stride < nseg) fetch(s + stride);
-    vst<real>(h + sx * KP + li * G::VE, seg_out(sgm, d1, x1, hs));
+    vst<real>(h + sx * KP + li * G::VE, seg_out(sgm, d1, x1, hs, nullptr));
   }
 }
 
@@ -3051,15 +3128,29 @@ __global__ __launch_bounds__(BLOCK) void k_gram_mfma32(uint64_t Rp, const float 
 // share its B rows in the Infinity Cache.  Partials: part[chunk][c * 4096 +
 // m * 64 + n] and the sums at [C * 4096 ..) (k_reduce_parts, fixed order).
 constexpr int GW64 = 1;  // tables per wave of k_gram_mfma64 (64 accumulators each)
+// XCD-aware block order (round 6).  Workgroups are dealt round-robin over
+// the 8 XCDs (blocks b and b + 8 share one, MI355X guide §Workgroup
+// dispatch), so the ngroups blocks of one row chunk — which all read that
+// chunk's B rows — landed on different XCDs and each XCD's L2 fetched B
+// again (config 5: 105.8 GB fetched per launch against 65.3 GB of tables).
+// With the grid a multiple of 8, work item L = (b % 8) * (grid / 8) + b / 8
+// gives each XCD a contiguous run of work items, so the blocks of a chunk
+// run on one XCD back to back and B is fetched into one L2 once.  Work items
+// past nwork (the padding) exit.
+__device__ __forceinline__ unsigned xcd_work_item(unsigned b, unsigned grid) {
+  return (b & 7u) * (grid >> 3) + (b >> 3);
+}
 static __global__ __launch_bounds__(BLOCK, 3) void k_gram_mfma64(uint64_t Rp, int C, const float *const *__restrict__ A,
                                                        const float *__restrict__ B, const float *__restrict__ wv,
                                                        float *__restrict__ part, uint64_t nout,
-                                                       uint64_t rows_per_block, unsigned ngroups) {
+                                                       uint64_t rows_per_block, unsigned ngroups, unsigned nwork) {
   typedef float f16x __attribute__((ext_vector_type(16)));
   constexpr int U = 4;  // row pairs per round (U = 8: 9 % slower at config 5)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int e = lane & 31, hf = lane >> 5;
-  const unsigned grp = blockIdx.x % ngroups, chunk = blockIdx.x / ngroups;
+  const unsigned L = (gridDim.x & 7u) ? blockIdx.x : xcd_work_item(blockIdx.x, gridDim.x);
+  if (L >= nwork) return;
+  const unsigned grp = L % ngroups, chunk = L / ngroups;
   const int c0 = (int)(grp * (BLOCK / 64) + w);
   if (c0 > C) return;  // no barrier below
   f16x acc[4];
@@ -3156,12 +3247,14 @@ static __global__ __launch_bounds__(BLOCK) void k_gram_mfma_f64(uint64_t Rp, int
                                                                const double *__restrict__ B,
                                                                const double *__restrict__ wv, double *__restrict__ part,
                                                                uint64_t nout, uint64_t rows_per_block,
-                                                               unsigned ngroups) {
+                                                               unsigned ngroups, unsigned nwork) {
   typedef double d4 __attribute__((ext_vector_type(4)));
   constexpr int U = 4;  // groups of four rows per register set
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c16 = lane & 15, rq = lane >> 4;
-  const unsigned grp = blockIdx.x % ngroups, chunk = blockIdx.x / ngroups;
+  const unsigned L = (gridDim.x & 7u) ? blockIdx.x : xcd_work_item(blockIdx.x, gridDim.x);  // (k_gram_mfma64)
+  if (L >= nwork) return;
+  const unsigned grp = L % ngroups, chunk = L / ngroups;
   const int c0 = (int)(grp * (BLOCK / 64) + w);
   if (c0 > C) return;  // no barrier below
   const uint64_t r0 = (uint64_t)chunk * rows_per_block;

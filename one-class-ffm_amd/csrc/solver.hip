@@ -1729,9 +1729,11 @@ template <typename real> class Problem final : public ProblemBase {
     nbx = std::max<uint64_t>(1, (Rp + rpb - 1) / rpb);
     if (gpart64_.n < nbx * nout) gpart64_.alloc(nbx * nout, false);
     const double abytes = (double)Rp * ((L + (B ? 1 : 0)) * 64 + (wv ? 1 : 0)) * sizeof(real);
+    const unsigned nwork = (unsigned)(nbx * gy);
+    const unsigned grid = xcd_order_ ? (nwork + 7) / 8 * 8 : nwork;  // whole rounds of the 8 XCDs (k_gram_mfma64)
     prof_launch("aggregates", abytes, [&] {
-      launch(k_gram_mfma64, (unsigned)(nbx * gy), BLOCK, 0, Rp, L, (const float *const *)A, (const float *)B,
-             (const float *)wv, gpart64_.p, nout, rpb, gy);
+      launch(k_gram_mfma64, grid, BLOCK, 0, Rp, L, (const float *const *)A, (const float *)B,
+             (const float *)wv, gpart64_.p, nout, rpb, gy, nwork);
     }, 2.0 * Rp * L * 64 * 64);
     const uint64_t ng = (uint64_t)L * 4096, cnt = ng + 129;
     prof_launch("aggr_reduce", (double)nbx * cnt * 4, [&] {
@@ -1752,9 +1754,11 @@ template <typename real> class Problem final : public ProblemBase {
     nbx = std::max<uint64_t>(1, (Rp + rpb - 1) / rpb);
     if (gpartd_.n < nbx * nout) gpartd_.alloc(nbx * nout, false);
     const double abytes = (double)Rp * ((L + 1) * 32 + (wv ? 1 : 0)) * sizeof(real);
+    const unsigned nwork = (unsigned)(nbx * gy);
+    const unsigned grid = xcd_order_ ? (nwork + 7) / 8 * 8 : nwork;
     prof_launch("aggregates", abytes, [&] {
-      launch(k_gram_mfma_f64, (unsigned)(nbx * gy), BLOCK, 0, Rp, L, (const double *const *)A, (const double *)B,
-             (const double *)wv, gpartd_.p, nout, rpb, gy);
+      launch(k_gram_mfma_f64, grid, BLOCK, 0, Rp, L, (const double *const *)A, (const double *)B,
+             (const double *)wv, gpartd_.p, nout, rpb, gy, nwork);
     }, 2.0 * Rp * L * 32 * 32);
     const uint64_t ng = (uint64_t)L * 1024, cnt = ng + 65;
     prof_launch("aggr_reduce", (double)nbx * cnt * 8, [&] {
@@ -3134,6 +3138,11 @@ template <typename real> class Problem final : public ProblemBase {
       int *errh = run_host_dev_ + MAXCG + 3, *abd = cgp_abort_.p;
       unsigned spin = cgp_spin_;
       int stall = cgp_stall_;
+      if (grid > resident(k_cg_cgram<real, KP>, 0)) {  // cannot be resident at once: per-step path
+        counters["cgp_refused"]++;
+        ok = false;
+        return;
+      }
       counters["cgp_launches"]++;
       prof_launch("cg_cgram", 0.0, [&] {
         if (!cgp_coop_) {
@@ -3284,18 +3293,28 @@ template <typename real> class Problem final : public ProblemBase {
           const size_t smem = lds ? qsz : 0;
           const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
                                (double)own.npos * 4 + (double)h.partner->R * KP * rs + (double)own.R * KP * rs;
+          // tau on the matrix cores (kernels.hpp TauTile) where the rows take
+          // it per row: fp32, QTQ in LDS, no column tau, no hot rows, segment order
+          const bool tt = tau_mfma_ && TauTile<real, KP>::OK && lds && !coltau(h) && !hot(h) && !sord(own);
           auto go = [&](auto ml) {
             constexpr bool ML = decltype(ml)::value;
             auto go2 = [&](auto pw) {
               constexpr int PW = decltype(pw)::value;
-              unsigned grid = grid_for(own.nseg, 4 * Gm::NSG, hs_blocks_);
-              if (row_fill_) grid = std::min(grid, resident(k_hs_cross_seg<real, KP, ML, PW>, smem));
-              launch(k_hs_cross_seg<real, KP, ML, PW>, grid, BLOCK, smem,
-                     own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.ycol.p, h.Q1,
-                     (uint64_t)h.partner->R, coltau(h) ? (const real *)nullptr : (const real *)qtq_, w_, h_.p, run,
-                     Rv_.p, Hv_.p, st_.p, it, F.segd.p, F.segx.p,
-                     hot(h) ? (const uint32_t *)own.hot_seg.p : (const uint32_t *)nullptr, (const real *)hotG_.p,
-                     sord(own));
+              auto go3 = [&](auto ttc) {
+                constexpr bool TT = decltype(ttc)::value && ML && TauTile<real, KP>::OK;
+                const size_t sm = TT ? TauTile<real, KP>::bytes() : smem;
+                unsigned grid = TT ? grid_for(own.nseg, TauTile<real, KP>::SB, hs_blocks_)
+                                   : grid_for(own.nseg, 4 * Gm::NSG, hs_blocks_);
+                if (row_fill_) grid = std::min(grid, resident(k_hs_cross_seg<real, KP, ML, PW, TT>, sm));
+                launch(k_hs_cross_seg<real, KP, ML, PW, TT>, grid, BLOCK, sm,
+                       own.nseg, own.segs.p, F.xptr.p, F.xidx.p, F.xval.p, Vd_.p, own.ycol.p, h.Q1,
+                       (uint64_t)h.partner->R, coltau(h) ? (const real *)nullptr : (const real *)qtq_, w_, h_.p, run,
+                       Rv_.p, Hv_.p, st_.p, it, F.segd.p, F.segx.p,
+                       hot(h) ? (const uint32_t *)own.hot_seg.p : (const uint32_t *)nullptr, (const real *)hotG_.p,
+                       sord(own));
+              };
+              if (tt) go3(std::true_type());
+              else go3(std::false_type());
             };
             if constexpr (Gm::LPR <= 16) {
               if (own.short_segs) {
@@ -3626,6 +3645,10 @@ template <typename real> class Problem final : public ProblemBase {
   bool no_mfma_ = std::getenv("OCFFM_NO_MFMA") != nullptr;  // Grams on the VALU kernel instead
   DevBuf<float> gpart64_;  // k_gram_mfma64 partials
   DevBuf<double> gpartd_;  // k_gram_mfma_f64 partials
+  // OCFFM_TAU_MFMA=0: the cross Hessian-vector row pass takes tau by sg_vecmat (VALU) instead of MFMA tiles
+  bool tau_mfma_ = !std::getenv("OCFFM_TAU_MFMA") || std::atoi(std::getenv("OCFFM_TAU_MFMA")) != 0;
+  // OCFFM_XCD_ORDER=0: the Gram kernels' blocks in plain order (no XCD-aware remap)
+  bool xcd_order_ = !std::getenv("OCFFM_XCD_ORDER") || std::atoi(std::getenv("OCFFM_XCD_ORDER")) != 0;
   uint64_t gram64_blocks_ = std::getenv("OCFFM_GRAM64_BLOCKS") ? std::strtoull(std::getenv("OCFFM_GRAM64_BLOCKS"), nullptr, 10) : 1024;
   uint64_t gram_blocks_ = std::getenv("OCFFM_GRAM_BLOCKS") ? std::strtoull(std::getenv("OCFFM_GRAM_BLOCKS"), nullptr, 10) : 512;
   bool no_owned_ = false;
@@ -3677,8 +3700,8 @@ template <typename real> class Problem final : public ProblemBase {
   DevBuf<int> cgp_abort_;  // 1: the last persistent grid gave up (guards its queued update)
   unsigned cgp_gen_ = 1, ncu_ = 256;
   bool cgp_on_ = !std::getenv("OCFFM_CGP") || std::atoi(std::getenv("OCFFM_CGP")) != 0;
-  // OCFFM_CGP_COOP=0: plain launch instead of the cooperative one
-  bool cgp_coop_ = !std::getenv("OCFFM_CGP_COOP") || std::atoi(std::getenv("OCFFM_CGP_COOP")) != 0;
+  // OCFFM_CGP_COOP=1: cooperative launch (the runtime's residency check; +0.27 ms per kkbox epoch)
+  bool cgp_coop_ = std::getenv("OCFFM_CGP_COOP") && std::atoi(std::getenv("OCFFM_CGP_COOP")) != 0;
   // tests: a short spin limit and one block stalled at a given step force the give-up
   unsigned cgp_spin_ = std::getenv("OCFFM_CGP_SPIN") ? (unsigned)std::atol(std::getenv("OCFFM_CGP_SPIN")) : CGP_SPIN_MAX;
   int cgp_stall_ = std::getenv("OCFFM_CGP_STALL") ? std::atoi(std::getenv("OCFFM_CGP_STALL")) : 0;

@@ -255,10 +255,31 @@ struct Problem {
     }
   }
 
+  // inner() = cblas_ddot (ffm.cpp:57-60).  Its summation order is the BLAS
+  // build's: serial here by default (dot_lanes = dot_chunks = 1).  For the
+  // drift envelope (tools/fp64_drift.py) the order of an optimised build can
+  // be restated: dot_chunks contiguous chunks (a threaded ddot) each summed in
+  // dot_lanes interleaved accumulators (SIMD registers: element i into lane
+  // i % lanes), the lanes reduced pairwise, the chunks added in order.
+  u32 dot_lanes = 1, dot_chunks = 1;
   double dot(const double *x, const double *y, u64 len) const {
-    double s = 0;
-    for (u64 i = 0; i < len; i++) s += x[i] * y[i];
-    return s;
+    if (dot_lanes <= 1 && dot_chunks <= 1) {
+      double s = 0;
+      for (u64 i = 0; i < len; i++) s += x[i] * y[i];
+      return s;
+    }
+    const u32 L = std::max<u32>(1, std::min<u32>(dot_lanes, 64));
+    const u64 nc = std::max<u64>(1, std::min<u64>(dot_chunks, len));
+    double tot = 0;
+    for (u64 c = 0; c < nc; c++) {
+      const u64 b = len * c / nc, e = len * (c + 1) / nc;
+      double acc[64] = {0};
+      for (u64 i = b; i < e; i++) acc[(i - b) % L] += x[i] * y[i];
+      for (u32 w = 1; w < L; w *= 2)
+        for (u32 l = 0; l + w < L; l += 2 * w) acc[l] += acc[l + w];
+      tot += acc[0];
+    }
+    return tot;
   }
 
   // ffm.cpp:334-350 + 467-512.
@@ -1060,6 +1081,13 @@ double orc_func(void *c) { return ((OrcCtx *)c)->prob.func(); }
 void orc_set_threads(void *c, uint32_t t) {
   ((OrcCtx *)c)->prob.prm.nr_threads = t;
   omp_set_num_threads((int)t);
+}
+
+// The ddot summation order of an optimised CBLAS (Problem::dot): lanes
+// interleaved accumulators over `chunks` contiguous chunks.  1, 1 = serial.
+void orc_set_dot_order(void *c, uint32_t lanes, uint32_t chunks) {
+  ((OrcCtx *)c)->prob.dot_lanes = lanes;
+  ((OrcCtx *)c)->prob.dot_chunks = chunks;
 }
 
 // out: [loss, prec@5..80, ndcg@5..80] (11 doubles).  per_row_ndcg

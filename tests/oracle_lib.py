@@ -51,6 +51,7 @@ def lib():
         L.orc_func.restype = C.c_double
         L.orc_func.argtypes = [C.c_void_p]
         L.orc_set_threads.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_set_dot_order.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
         L.orc_validate.argtypes = [C.c_void_p, C.c_int, _f64p, C.c_void_p, C.c_uint64]
         L.orc_validate.restype = C.c_uint64
         L.orc_cg_log.restype = C.c_int
@@ -198,6 +199,12 @@ class Oracle:
 
     def save_binary(self, path):
         lib().orc_save_binary(self.h, path.encode())
+
+    def set_dot_order(self, lanes, chunks=1):
+        """Sum the cblas_ddot restatement (inner(), ffm.cpp:57-60) in the
+        order of an optimised BLAS build: `lanes` interleaved accumulators
+        over `chunks` contiguous chunks (1, 1: serial, the default)."""
+        lib().orc_set_dot_order(self.h, lanes, chunks)
 
     def time_epochs(self, epochs, threads=None):
         if threads is not None:

@@ -632,19 +632,27 @@ def test_kkbox_full_size_parity_fp64(kk_full):
     epochs from the same srand(1) init.  Every table of every block, both
     biases and both y~ orientations within max(1e-9, 3x the reference
     arithmetic's own drift at this size: the oracle at 2..16 threads against
-    1 thread, fp64_envelope.json "kkbox_full"); CG logs identical;
-    validate() (ffm.cpp:925-1016) on the test split: loss within 1e-9,
-    p@k / nDCG@k within 1e-9."""
+    1 thread serial, and at 8 threads with the cblas_ddot orders of optimised
+    BLAS builds, fp64_envelope.json "kkbox_full": 3.7e-9 / 8.5e-7 after
+    epochs 1 / 2; the CG scalars' ddot order, which no thread count changes,
+    is what the song-id and artist halves' 7-13-step solves amplify); CG
+    logs identical; validate() (ffm.cpp:925-1016) on the test split after
+    each epoch: loss within the same bound, p@k / nDCG@k within 1e-9 after
+    epoch 1 and, after epoch 2, within two test rows' worth (2 / m_te: a
+    near-tie in a top-k list may order the other way at 1e-6)."""
     o, g = _full_pair(kk_full, ocffm.FP64)
+    mt = kk_full.test.m
     for e in (1, 2):
         o.one_epoch()
         g.one_epoch()
-        assert_state(o, g, fp64_tol("kkbox_full", e))
+        tol = fp64_tol("kkbox_full", e)
+        assert_state(o, g, tol)
         np.testing.assert_array_equal(g.cg_log(), o.cg_log())
-    vo, vg = o.validate(), g.validate()
-    assert abs(vg["loss"] - vo["loss"]) <= 1e-9 * abs(vo["loss"])
-    np.testing.assert_allclose(vg["prec"], vo["prec"], atol=1e-9)
-    np.testing.assert_allclose(vg["ndcg"], vo["ndcg"], atol=1e-9)
+        vo, vg = o.validate(), g.validate()
+        assert abs(vg["loss"] - vo["loss"]) <= tol * abs(vo["loss"]), (e, vg["loss"], vo["loss"])
+        atol = 1e-9 if e == 1 else 2.0 / mt
+        np.testing.assert_allclose(vg["prec"], vo["prec"], atol=atol, err_msg=f"epoch {e}")
+        np.testing.assert_allclose(vg["ndcg"], vo["ndcg"], atol=atol, err_msg=f"epoch {e}")
 
 
 def test_kkbox_full_size_parity_fp32(kk_full):

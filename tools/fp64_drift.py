@@ -17,7 +17,10 @@ every block, a, b, both y~ orientations) of each run against the 1-thread oracle
     python tools/fp64_drift.py [epochs] --envelope tests/golden/fp64_envelope.json [--sets a,b]
 
 --envelope (CPU only): the oracle at 2, 3, 4, 6, 8 and 16 threads, twice
-each; per set and epoch the largest drift from the 1-thread run is the
+each, and at 8 threads with its cblas_ddot restatement summed in the orders
+of optimised BLAS builds (SIMD accumulators, a threaded ddot's chunks:
+ffm.cpp:57-60 calls cblas_ddot, whose order the BLAS build decides; round 6);
+per set and epoch the largest drift from the 1-thread serial run is the
 envelope of the reference's own arithmetic, which the GPU parity tests use
 as their bound where it exceeds 1e-9 (tests/test_gpu_parity.py fp64_tol).
 """
@@ -71,8 +74,10 @@ def state(x, o=None):
     return st
 
 
-def run_oracle(ds, kw, threads, E):
+def run_oracle(ds, kw, threads, E, dot=None):
     o = O.Oracle(ds, threads=threads, with_test=False, **kw)
+    if dot:
+        o.set_dot_order(*dot)
     O.lib().orc_srand(1)
     o.init()
     st = []
@@ -102,6 +107,9 @@ def run_gpu(ds, kw, E, exact):
     return st, cg
 
 
+BLAS_ORDERS = [(4, 1), (16, 1), (32, 1), (16, 8), (16, 16)]
+
+
 def envelope(E, path, only=None):
     res = {}
     E_file = E
@@ -115,16 +123,23 @@ def envelope(E, path, only=None):
         ds = mk()
         ref, cg1, _ = run_oracle(ds, kw, 1, E)
         env = [0.0] * E
-        for th in (2, 3, 4, 6, 8, 16):
-            for _ in range(2):
-                st, cg, _ = run_oracle(ds, kw, th, E)
-                assert np.array_equal(cg, cg1), (name, th)
-                env = [max(env[e], max(rel(st[e][key], ref[e][key]) for key in ref[e])) for e in range(E)]
+        runs = [(th, None) for th in (2, 3, 4, 6, 8, 16) for _ in range(2)]
+        # the cblas_ddot order of optimised BLAS builds (Problem::dot): SIMD
+        # accumulators (AVX2: 16 doubles in flight, AVX-512: 32), a threaded
+        # ddot's contiguous chunks
+        runs += [(8, dot) for dot in BLAS_ORDERS]
+        for th, dot in runs:
+            st, cg, _ = run_oracle(ds, kw, th, E, dot)
+            assert np.array_equal(cg, cg1), (name, th, dot)
+            env = [max(env[e], max(rel(st[e][key], ref[e][key]) for key in ref[e])) for e in range(E)]
         res[name] = env
         print(f"{name:11s} " + " ".join(f"{x:.2e}" for x in env), flush=True)
     with open(path, "w") as f:
         json.dump({"epochs": E_file, "threads": [2, 3, 4, 6, 8, 16], "repeats": 2,
-                   "what": "max relative difference (W, H, P, Q, a, b, y~) of the oracle at T threads vs 1 thread, per epoch",
+                   "blas_orders": [list(x) for x in BLAS_ORDERS],
+                   "what": "max relative difference (W, H, P, Q, a, b, y~) of the oracle at T threads, and with the "
+                           "ddot orders of optimised BLAS builds (lanes, chunks) at 8 threads, vs 1 thread serial, "
+                           "per epoch",
                    "sets": res}, f, indent=1)
 
 

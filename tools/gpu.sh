@@ -7,7 +7,7 @@
 #   smoke           __graft_entry__.smoke()
 #   bench[=ARGS]    python bench.py ARGS (default: the driver's command), gpurun_out/<tag>_bench.json
 #   prof=WHAT       rocprofv3 stats + FETCH/WRITE passes (tools/run_profiles.sh WHAT: kkbox fp64 cfg5 kdd12 outbrain)
-#   ab=N:ENV_A:ENV_B  N alternations of two env settings (tools/ab.sh), gpurun_out/<tag>_ab.txt
+#   ab=N:ENV_A:ENV_B[:...]  N alternations of env settings (tools/ab.sh; "OCFFM_X=1" = none), gpurun_out/<tag>_ab.txt
 #   pe=ARGS         tools/profile_epoch.py ARGS (per-half timeline)
 #   py=SCRIPT       python SCRIPT (an experiment script under tools/)
 set -e -o pipefail
@@ -38,8 +38,8 @@ for step in "$@"; do
     prof)
       bash tools/run_profiles.sh $tag $arg;;
     ab)
-      IFS=: read -r n ea eb <<< "$arg"
-      bash tools/ab.sh $n "$ea" "$eb" "OCFFM_X=1"
+      IFS=: read -r -a parts <<< "$arg"
+      bash tools/ab.sh "${parts[@]}"
       cp $out/ab.txt $out/${tag}_ab.txt;;
     pe)
       timeout -k 10 600 python tools/profile_epoch.py $arg > $out/${tag}_pe.txt 2>&1

@@ -85,6 +85,9 @@ constexpr int BLOCK = 256;   // 4 waves
 // entering pass came out at 172 + 4 registers, 2 waves; bounded: 166, no spill)
 #define OCFFM_GD_OCC 3
 #endif
+#ifndef OCFFM_GD_OCC_IN
+#define OCFFM_GD_OCC_IN OCFFM_GD_OCC  // the fp32 passes with one gather per positive (BM_IN, BM_FULL)
+#endif
 #ifndef OCFFM_GD_OCC64
 // the fp64 build of k_gd_cross_seg: wide lanes bounded to 3 waves per SIMD
 // (the entering pass: 167 registers), else the compiler's choice
@@ -1109,7 +1112,7 @@ template <typename real, int KP> struct TMma {
 };
 
 template <typename real, int KP, bool MLDS, int BM, bool TP = false, bool PRB = false>
-__global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_GD_OCC64 : OCFFM_GD_OCC) void k_gd_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
+__global__ __launch_bounds__(BLOCK, sizeof(real) == 8 ? OCFFM_GD_OCC64 : (BM == BM_ENTER ? OCFFM_GD_OCC : OCFFM_GD_OCC_IN)) void k_gd_cross_seg(uint64_t nseg, const Seg *__restrict__ segs,
                                                         const uint32_t *__restrict__ ycol,
                                                         real *__restrict__ yt, const real *__restrict__ Q1,
                                                         int C, const real *const *__restrict__ Ptabs,
@@ -2725,6 +2728,26 @@ __device__ __forceinline__ vec_t<real> apply_owned_row(const real *__restrict__ 
   return s;
 }
 
+// k_apply's work folded into an update kernel for a field that is not
+// id-like (round 6): the rows form XS from the final step S + a p
+// on the fly (the same expression k_apply stores), and every thread of the
+// grid then takes a stride of W += S + a p.  Nothing in the kernel reads W,
+// and S is only read, so the two parts need no ordering.  nv = D KP / VE
+// (0: no fold).
+template <typename real>
+__device__ __forceinline__ vec_t<real> final_step(const real *__restrict__ S, const real *__restrict__ Pd, real alpha,
+                                                  size_t off) {
+  return vld<real>(S + off) + vsplat<real>(alpha) * vld<real>(Pd + off);
+}
+template <typename real>
+__device__ __forceinline__ void fold_apply(uint64_t nv, const real *__restrict__ S, const real *__restrict__ Pd,
+                                           real *__restrict__ W, real alpha) {
+  for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < nv; v += (uint64_t)gridDim.x * BLOCK) {
+    const vec_t<real> s = final_step<real>(S, Pd, alpha, v * VT<real>::N);
+    vst<real>(W + v * VT<real>::N, vld<real>(W + v * VT<real>::N) + s);
+  }
+}
+
 // Per segment of row i (one segment per subgroup): XS_i = X_i S;
 // [first] P_i += XS_i; base_ij += <XS_i, q_j> for the segment's positives
 // (update_cross, ffm.cpp:439-465), in this side's orientation; k_gather_pos
@@ -2820,15 +2843,18 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_rows(uint64_t R, const i
                                                              const real *__restrict__ S, real *__restrict__ P1,
                                                              real *__restrict__ XS, bool one, real *__restrict__ W,
                                                              const real *__restrict__ Pd, const CgState *st,
-                                                             const int *__restrict__ skip) {
+                                                             const int *__restrict__ skip, uint64_t nfold) {
   using G = Geo<real, KP>;
   if (skip && *skip) return;
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
-  const real alpha = (W && st->nr_cg >= 1) ? (real)st->alpha : (real)0;
+  const real alpha = ((W || nfold) && st->nr_cg >= 1) ? (real)st->alpha : (real)0;
   for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
     vec_t<real> xs = vzero<real>();
-    if (W) {
+    if (nfold) {  // W is updated below (fold_apply): S + a p on the fly
+      for (int64_t p = one ? (int64_t)i : xptr[i]; p < (one ? (int64_t)i + 1 : xptr[i + 1]); p++)
+        xs += vsplat<real>(xval[p]) * final_step<real>(S, Pd, alpha, (size_t)xidx[p] * KP + li * G::VE);
+    } else if (W) {
       xs = vsplat<real>(xval[i]) * apply_owned_row<real, KP>(S, Pd, W, alpha, (size_t)xidx[i] * KP + li * G::VE);
     } else if (one) {
       xs = vsplat<real>(xval[i]) * vld<real>(S + (size_t)xidx[i] * KP + li * G::VE);
@@ -2839,6 +2865,7 @@ __global__ __launch_bounds__(BLOCK) void k_update_cross_rows(uint64_t R, const i
     vst<real>(P1 + i * KP + li * G::VE, vld<real>(P1 + i * KP + li * G::VE) + xs);
     if (XS) vst<real>(XS + i * KP + li * G::VE, xs);
   }
+  if (nfold) fold_apply<real>(nfold, S, Pd, W, alpha);
 }
 
 // dst[q] = src[idx[q]]: the other orientation of base from this one (idx =
@@ -2878,16 +2905,19 @@ __global__ __launch_bounds__(BLOCK) void k_update_side_row(uint64_t R, const int
                                                            real *__restrict__ a1, bool one, real *__restrict__ W,
                                                            const real *__restrict__ Pd, const CgState *st,
                                                            double *__restrict__ asum, double *part, unsigned *tick,
-                                                           const int *__restrict__ skip) {
+                                                           const int *__restrict__ skip, uint64_t nfold) {
   using G = Geo<real, KP>;
   if (skip && *skip) return;  // (every block: the last_block tickets stay untouched)
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
-  const real alpha = (W && st->nr_cg >= 1) ? (real)st->alpha : (real)0;
+  const real alpha = ((W || nfold) && st->nr_cg >= 1) ? (real)st->alpha : (real)0;
   double bs = 0;
   for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
     vec_t<real> xs = vzero<real>();
-    if (W) {  // id-like: one node per row, the row owns its feature
+    if (nfold) {  // W is updated below (fold_apply): S + a p on the fly
+      for (int64_t p = one ? (int64_t)i : xptr[i]; p < (one ? (int64_t)i + 1 : xptr[i + 1]); p++)
+        xs += vsplat<real>(xval[p]) * final_step<real>(S, Pd, alpha, (size_t)xidx[p] * KP + li * G::VE);
+    } else if (W) {  // id-like: one node per row, the row owns its feature
       xs = vsplat<real>(xval[i]) * apply_owned_row<real, KP>(S, Pd, W, alpha, (size_t)xidx[i] * KP + li * G::VE);
     } else if (one) {
       xs = vsplat<real>(xval[i]) * vld<real>(S + (size_t)xidx[i] * KP + li * G::VE);
@@ -2903,6 +2933,7 @@ __global__ __launch_bounds__(BLOCK) void k_update_side_row(uint64_t R, const int
       bs += (double)an;
     }
   }
+  if (nfold) fold_apply<real>(nfold, S, Pd, W, alpha);
   const double bv[1] = {block_sum(bs)};
   double tot[1];
   if (last_block<1>(bv, part, tick, tot) && threadIdx.x == 0) asum[0] = tot[0];

@@ -526,6 +526,10 @@ template <typename real> class Problem final : public ProblemBase {
     if (stage_) (void)hipHostFree(stage_);
     if (dstage_) (void)hipHostFree(dstage_);
     for (auto &e : ev_pool_) (void)hipEventDestroy(e);
+    if (side_) (void)hipStreamSynchronize(side_);
+    if (side_ev_[0]) (void)hipEventDestroy(side_ev_[0]);
+    if (side_ev_[1]) (void)hipEventDestroy(side_ev_[1]);
+    if (side_) (void)hipStreamDestroy(side_);
     if (stream_) (void)hipStreamDestroy(stream_);
     if (comm_.nccl) ncclCommDestroy(comm_.nccl);
   }
@@ -534,7 +538,10 @@ template <typename real> class Problem final : public ProblemBase {
   uint64_t test_rows() const override { return has_test_ ? T_.R : 0; }
   uint32_t nr_pass() const override { return prm_.nr_pass; }
   int rank() const override { return comm_.rank; }
-  void sync() override { HIPCHK(hipStreamSynchronize(stream_)); }
+  void sync() override {
+    side_join();
+    HIPCHK(hipStreamSynchronize(stream_));
+  }
 
   // FNV-1a digests of every array of the data layout (and its counts), in
   // a fixed order: the device build and the host build must agree on each.
@@ -1971,7 +1978,10 @@ template <typename real> class Problem final : public ProblemBase {
         if (enter) bytes += (double)own.npos * rs + (dxs ? (double)ps.R * KP * rs : 0);
         // inside the block (BM_IN): read the stored value through perm from
         // the orientation the entering pass wrote (no refresh in between)
-        const bool via = ytvia_ && cur && !enter;
+        const bool via = ytvia_ && cur && !enter && !side_pending_;
+        // the item orientation refreshed on the side stream (side_refresh_):
+        // the in-block pass reads it in order once the refresh has landed
+        if (cur && !enter) side_join();
         // T_i = sum_c P_c[i] M_c on MFMA ahead of the pass (k_rows_T), where
         // the C Grams do not fit the pass's LDS (or OCFFM_TPRE=1)
         const bool tp = tpre(own.R, own.npos);
@@ -2035,9 +2045,26 @@ template <typename real> class Problem final : public ProblemBase {
           if (lds && !tp) go(std::true_type());
           else go(std::false_type());
         });
-        // the other orientation: refreshed here, or read through perm by the
-        // block's second half (ytvia_; flush_base refreshes it after the loop)
-        if (enter && !ytvia_) refresh_other(own, *h.partner);
+        // the other orientation: refreshed here, or on the side stream while
+        // this half's CG runs (side_refresh_: nothing reads it before the
+        // block's second half), or read through perm by the block's second
+        // half (ytvia_; flush_base refreshes it after the loop)
+        if (enter && side_refresh_ && h.partner->npos) {
+          if (!side_) {
+            HIPCHK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&side_ev_[0], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&side_ev_[1], hipEventDisableTiming));
+          }
+          HIPCHK(hipEventRecord(side_ev_[0], stream_));
+          HIPCHK(hipStreamWaitEvent(side_, side_ev_[0], 0));
+          std::swap(stream_, side_);  // launch() and the profiler's events go to the stream in stream_
+          refresh_other(own, *h.partner);
+          std::swap(stream_, side_);
+          HIPCHK(hipEventRecord(side_ev_[1], side_));
+          side_pending_ = true;
+        } else if (enter && !ytvia_) {
+          refresh_other(own, *h.partner);
+        }
         // QTQ for CG = M of this block (M_ is not rewritten before the half ends)
         const uint32_t c0 = cross_slot(std::min(h.fl, h.fo), std::max(h.fl, h.fo));
         qtq_ = M_.p + (size_t)c0 * KP * KP;
@@ -2076,7 +2103,14 @@ template <typename real> class Problem final : public ProblemBase {
   // Restore the full base from the block-excluded y~:
   // base_ij = e_ij + <P_b[i], Q_b[j]> - a_i - b_j in the user orientation
   // (k_update_cross_seg with XS = P_b), then the refresh of the other one.
+  // the main stream waits for a pending side-stream refresh (side_refresh_)
+  void side_join() {
+    if (!side_pending_) return;
+    HIPCHK(hipStreamWaitEvent(stream_, side_ev_[1], 0));
+    side_pending_ = false;
+  }
   void flush_base() {
+    side_join();
     if (!excl_.on) return;
     ysum_dirty();
     excl_.on = false;
@@ -3488,8 +3522,15 @@ template <typename real> class Problem final : public ProblemBase {
       // kernel (apply_owned_row), one launch fewer at the end of the half
       DevField<real> &F = *h.F;
       const bool fold = F.idlike && own.R > 0 && !excl && !no_fold_;
-      real *Wf = fold ? h.W1 : nullptr;
-      if (!fold)
+      // any other field on one rank's rows kernel: k_apply folded in too
+      // (kernels.hpp fold_apply: W += S + a p by a grid stride, the rows
+      // form XS from S + a p), one launch fewer per half
+      const bool rows_kernel = !h.cross || (excl_.on && excl_.b12 == h.b12);
+      const bool gfold = !fold && own.R > 0 && !excl && !no_fold_ && gfold_on_ && rows_kernel;
+      real *Wf = (fold || gfold) ? h.W1 : nullptr;
+      const uint64_t nfold = gfold ? nv : 0;
+      const double fbytes = gfold ? (double)h.D * KP * rs * 4 : 0.0;
+      if (!fold && !gfold)
         prof_launch("apply_step", (double)h.D * KP * rs * 5, [&] {
           launch(k_apply<real>, grid_for(nv, BLOCK, 2048), BLOCK, 0, nv, Vd_.p, S_.p, h.W1, st_.p,
                  excl ? (const uint8_t *)h.F->own.p : nullptr, (uint32_t)Gm::LPR, skip);
@@ -3500,10 +3541,10 @@ template <typename real> class Problem final : public ProblemBase {
         if (excl_.on && excl_.b12 == h.b12) {
           // block-excluded base: the base does not depend on P1, no positive pass
           prof_launch("update_cross_rows", (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
-                                               (double)own.R * KP * rs * 2, [&] {
+                                               (double)own.R * KP * rs * 2 + fbytes, [&] {
             launch(k_update_cross_rows<real, KP>, mfill(k_update_cross_rows<real, KP>, grid_for(own.R, 4 * Gm::NSG)), BLOCK, 0, own.R, F.xptr.p, F.xidx.p,
                    F.xval.p, (const real *)S_.p, h.P1, (real *)nullptr, F.one, Wf, (const real *)Vd_.p,
-                   (const CgState *)st_.p, skip);
+                   (const CgState *)st_.p, skip, nfold);
           });
           return;
         }
@@ -3521,11 +3562,11 @@ template <typename real> class Problem final : public ProblemBase {
       } else {
         DevSide<real> &other = h.user ? V_ : U_;
         const double bytes = (double)own.R * 16 + (double)F.nnz * (4 + rs) + (double)F.D * KP * rs +
-                             (double)own.R * KP * rs * 3 + (double)own.R * rs * 2 + (double)own.npos * (4 + 4 * rs);
+                             (double)own.R * KP * rs * 3 + (double)own.R * rs * 2 + (double)own.npos * (4 + 4 * rs) + fbytes;
         prof_launch("update_side_row", bytes, [&] {
           launch(k_update_side_row<real, KP>, mfill(k_update_side_row<real, KP>, grid_for(own.R, 4 * Gm::NSG)), BLOCK, 0,
               own.R, F.xptr.p, F.xidx.p, F.xval.p, S_.p, h.P1, h.Q1, own.bias.p, F.one, Wf,
-              (const real *)Vd_.p, (const CgState *)st_.p, bsum_.p + (h.user ? 0 : 1), part_.p, tick_.p, skip);
+              (const real *)Vd_.p, (const CgState *)st_.p, bsum_.p + (h.user ? 0 : 1), part_.p, tick_.p, skip, nfold);
         });
       }
     });
@@ -3587,7 +3628,16 @@ template <typename real> class Problem final : public ProblemBase {
   // Cross loop: the item halves read the block-excluded value through perm
   // from the user orientation (k_gd_cross_seg ytv) instead of a refresh after
   // each entering pass.  OCFFM_YTVIA=0: refresh.
+  // OCFFM_GFOLD=0: k_apply as its own launch for fields that are not id-like
+  bool gfold_on_ = !std::getenv("OCFFM_GFOLD") || std::atoi(std::getenv("OCFFM_GFOLD")) != 0;
   bool ytvia_ = !std::getenv("OCFFM_YTVIA") || std::atoi(std::getenv("OCFFM_YTVIA")) != 0;
+  // OCFFM_SIDE_REFRESH=1: the entering pass's refresh of the item orientation
+  // runs on a second stream, overlapped with the user half's CG; the block's
+  // item half then reads the stored value in order (no perm gather)
+  bool side_refresh_ = std::getenv("OCFFM_SIDE_REFRESH") && std::atoi(std::getenv("OCFFM_SIDE_REFRESH")) != 0;
+  hipStream_t side_ = nullptr;
+  hipEvent_t side_ev_[2] = {nullptr, nullptr};
+  bool side_pending_ = false;
   // T_i of the cross gradient passes precomputed on MFMA (k_rows_T; fp32,
   // KP = 32 or 64).  On where the C cross Grams exceed the pass's 64 KB of
   // LDS (BASELINE config 5: 39 Grams of 64 x 64, 624 KB: the pass would read

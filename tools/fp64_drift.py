@@ -62,6 +62,8 @@ SETS = {
     # the headline configuration at its own size (30,755 x 100,000, k = 32,
     # 2.1 M positives; tests/test_gpu_parity.py test_kkbox_full_size_parity_fp64)
     "kkbox_full": (lambda: synth.kkbox(test_frac=0.05), dict()),
+    # config 2 at its own size (500 k x 50 k, k = 16; test_kdd12_full_size_parity_fp64)
+    "kdd12_full": (lambda: synth.kdd12(test_rows=500), dict()),
 }
 
 
@@ -111,11 +113,12 @@ BLAS_ORDERS = [(4, 1), (16, 1), (32, 1), (16, 8), (16, 16)]
 
 
 def envelope(E, path, only=None):
-    res = {}
+    res, cg_res = {}, {}
     E_file = E
     if only and os.path.exists(path):  # add / refresh some sets of an existing envelope
         prev = json.load(open(path))
         res = prev["sets"]
+        cg_res = prev.get("cg_differs", {})
         E_file = max(E, prev.get("epochs", E))
     for name, (mk, kw) in SETS.items():
         if only and name not in only:
@@ -128,19 +131,27 @@ def envelope(E, path, only=None):
         # accumulators (AVX2: 16 doubles in flight, AVX-512: 32), a threaded
         # ddot's contiguous chunks
         runs += [(8, dot) for dot in BLAS_ORDERS]
+        cgdiff = 0  # halves whose CG count differs from the 1-thread serial run (the worst variant)
         for th, dot in runs:
             st, cg, _ = run_oracle(ds, kw, th, E, dot)
-            assert np.array_equal(cg, cg1), (name, th, dot)
+            nd = int(np.sum(cg != cg1)) if cg.shape == cg1.shape else len(cg1)
+            if nd:
+                print(f"  {name}: {nd} CG count(s) differ at {th} threads, ddot order {dot}", flush=True)
+            cgdiff = max(cgdiff, nd)
             env = [max(env[e], max(rel(st[e][key], ref[e][key]) for key in ref[e])) for e in range(E)]
         res[name] = env
-        print(f"{name:11s} " + " ".join(f"{x:.2e}" for x in env), flush=True)
+        if cgdiff:
+            cg_res[name] = cgdiff
+        print(f"{name:11s} " + " ".join(f"{x:.2e}" for x in env) + (f"  cg differs in {cgdiff} halves" if cgdiff else ""),
+              flush=True)
     with open(path, "w") as f:
         json.dump({"epochs": E_file, "threads": [2, 3, 4, 6, 8, 16], "repeats": 2,
                    "blas_orders": [list(x) for x in BLAS_ORDERS],
                    "what": "max relative difference (W, H, P, Q, a, b, y~) of the oracle at T threads, and with the "
                            "ddot orders of optimised BLAS builds (lanes, chunks) at 8 threads, vs 1 thread serial, "
                            "per epoch",
-                   "sets": res}, f, indent=1)
+                   "sets": res,
+                   "cg_differs": cg_res}, f, indent=1)
 
 
 def main():

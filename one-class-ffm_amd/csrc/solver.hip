@@ -629,6 +629,15 @@ template <typename real> class Problem final : public ProblemBase {
     // block-excluded form on: the base is rebuilt below from scratch
     excl_ = ExclBase{};
     lazy_ok_ = false;
+    // grid-reduction tickets and the persistent CG's words back at rest,
+    // whatever a failed call left (every kernel resets what it takes, so
+    // this only matters after an error the host reported mid-half)
+    side_join();
+    HIPCHK(hipMemsetAsync(tick_.p, 0, tick_.bytes(), stream_));
+    HIPCHK(hipMemsetAsync(cgp_abort_.p, 0, sizeof(int), stream_));
+    HIPCHK(hipMemsetAsync(cgp_gen_buf_.p, 0, sizeof(unsigned), stream_));
+    cgp_gen_ = 1;
+    run_host_[MAXCG + 3] = 0;
     tmark(nullptr);
     const size_t rs = sizeof(real);
     std::vector<double> host;

@@ -150,6 +150,9 @@ def run_newton(ds, prec, steps, warmup, k=32, self_side=True, world=1, rank=0, l
         g.one_epoch()
     barrier()
     ks = g.kernel_stats()
+    # persistent column-Gram CG launches and the ones whose grid gave up on
+    # its barrier and finished per step (ocffm_problem_counter)
+    cgp = {"launches": g.counter("cgp_launches"), "recovered": g.counter("cgp_recovered")}
     g.close()
 
     fams = {kk: v for kk, v in ks.items() if not kk.startswith("half(") and not kk.endswith(".noop")}
@@ -202,7 +205,7 @@ def run_newton(ds, prec, steps, warmup, k=32, self_side=True, world=1, rank=0, l
     # item-owned CG steps' row pass appears in the kernel-timing pass
     io_launches = int(ks.get("hs_cross_io", {}).get("launches", 0))
     return dict(dt=dt, roof=roof, cg_per_epoch=round(cg.sum() / max(1, steps), 1),
-                setup_s={"create": round(t_create, 3), "init": round(t_init, 3)}, io_launches=io_launches)
+                setup_s={"create": round(t_create, 3), "init": round(t_init, 3)}, io_launches=io_launches, cgp=cgp)
 
 
 T_START = time.perf_counter()
@@ -309,6 +312,7 @@ def main():
                        # launches of their row pass in the kernel-timing pass
                        "item_owned_cg": r["io_launches"] > 0,
                        "item_owned_cg_launches": r["io_launches"],
+                       "persistent_cg": r["cgp"],
                        "cg_iters_per_epoch": r["cg_per_epoch"]},
             "roofline": r["roof"],
             "cpu_baseline": cpu,

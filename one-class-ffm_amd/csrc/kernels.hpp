@@ -461,7 +461,7 @@ constexpr int TICK_WORDS = (TICK_SUB + 1) * TICK_STRIDE;
 // extra (optional): nextra x NV more values, stored by waves of any block
 // before their block's ticket (sc1 stores, drained), added to the total in
 // index order by the last block.
-template <int NV>
+template <int NV, int ROUND = 8>  // ROUND: blocks per thread per read-back round (registers: 2 ROUND NV)
 __device__ __forceinline__ bool last_block(const double (&v)[NV], double *part, unsigned *tick, double (&tot)[NV],
                                            const double *extra = nullptr, uint32_t nextra = 0) {
   __shared__ int s_last;
@@ -492,7 +492,6 @@ __device__ __forceinline__ bool last_block(const double (&v)[NV], double *part, 
   double x[NV];
 #pragma unroll
   for (int k = 0; k < NV; k++) x[k] = 0;
-  constexpr int ROUND = 8;  // blocks per thread per round
   for (unsigned b0 = 0; b0 < gridDim.x; b0 += ROUND * BLOCK) {
     double y[ROUND][NV];
 #pragma unroll
@@ -534,6 +533,19 @@ __device__ __forceinline__ bool last_block(const double (&v)[NV], double *part, 
   for (int k = 0; k < NV; k++) tot[k] = block_sum(x[k]);
   if (threadIdx.x == 0) __hip_atomic_store(tick, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
+}
+
+// XCD-aware block order (round 6).  Workgroups are dealt round-robin over
+// the 8 XCDs (blocks b and b + 8 share one, MI355X guide §Workgroup
+// dispatch), so the ngroups blocks of one row chunk — which all read that
+// chunk's B rows — landed on different XCDs and each XCD's L2 fetched B
+// again (config 5: 105.8 GB fetched per launch against 65.3 GB of tables).
+// With the grid a multiple of 8, work item L = (b % 8) * (grid / 8) + b / 8
+// gives each XCD a contiguous run of work items, so the blocks of a chunk
+// run on one XCD back to back and B is fetched into one L2 once.  Work items
+// past nwork (the padding) exit.
+__device__ __forceinline__ unsigned xcd_work_item(unsigned b, unsigned grid) {
+  return (b & 7u) * (grid >> 3) + (b >> 3);
 }
 
 #define WAVE_SETUP                                                                  \
@@ -2251,6 +2263,180 @@ __global__ __launch_bounds__(BLOCK) void k_cg_cgram(uint64_t D, const real *__re
   }
 }
 
+// The release / give-up barrier of the persistent CG kernels (k_cg_cgram
+// above; k_cg_side_id below), run by every block after its share of step
+// `it`: the last-arriving block publishes the CG scalars of the step
+// (cg_publish MODE 1, ffm.cpp:803-809, through agent-scope stores) and
+// releases the grid; the others wait (see the co-residency notes above).
+// Returns false when the grid gave up (every block then leaves).
+template <typename real>
+__device__ __forceinline__ bool cgp_step_end(const Fin<real> &f, const double (&dsum)[3], int it, unsigned *gen,
+                                             unsigned gen0, int *err_host, int *abort_dev, unsigned spin_max) {
+  __shared__ int s_ok;
+  CgState *st = f.st;
+  double bv[3] = {block_sum(dsum[0]), block_sum(dsum[1]), block_sum(dsum[2])}, tot[3];
+  if (last_block<3, 1>(bv, f.part, f.tick, tot)) {  // (a short read-back round: the caller holds state in registers)
+    if (threadIdx.x == 0) {
+      const double r2 = ald(&st->r2), g2 = ald(&st->g2);
+      const double a = r2 / tot[0];
+      const double r2n = r2 - 2 * a * tot[1] + a * a * tot[2];
+      ast(&st->vhv, tot[0]);
+      ast(&st->alpha, a);
+      ast(&st->beta, r2n / r2);
+      ast(&st->r2, r2n);
+      ast(&st->nr_cg, it);
+      const int go = (it < MAXCG && g2 * CG_EPS < r2n) ? 1 : 0;
+      ast(&st->run[it + 1], go);
+      if (f.run_host)
+        __hip_atomic_store(f.run_host + it + 1, go ? RUN_GO : RUN_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (OCFFM_CGP_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      unsigned cur = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int ok = 0;
+      while (cur != CGP_ABORT) {
+        if (__hip_atomic_compare_exchange_strong(gen, &cur, gen0 + (unsigned)it, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          ok = 1;
+          break;
+        }
+      }
+      if (!ok) cgp_report_abort(err_host, abort_dev, it);
+      s_ok = ok;
+    }
+  } else if (threadIdx.x == 0) {
+    int ok = 1;
+    unsigned spins = 0;
+    for (;;) {
+      unsigned cur = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == gen0 + (unsigned)it) {
+        if constexpr (OCFFM_CGP_FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        break;
+      }
+      if (cur == CGP_ABORT) {
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > spin_max &&
+          __hip_atomic_compare_exchange_strong(gen, &cur, CGP_ABORT, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)) {
+        cgp_report_abort(err_host, abort_dev, it);
+        ok = 0;
+        break;
+      }
+    }
+    s_ok = ok;
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
+// Persistent CG of a side half over an id-like field (round 6): every
+// CG step of the half in ONE launch with the CG vectors in registers.  An
+// id-like field's Hessian-vector product is row-local (row i is column
+// xidx[i]'s only row: hs_side, ffm.cpp:594-628, is k_hs_side_row FUSE's
+// d_i <x p, q_i> x q_i), so a block that owns a set of rows owns their
+// columns' p, r, Hp and S for the whole solve: the steps read no vector
+// from memory, only the CG scalars.  Block L (XCD-ordered) owns rows
+// [L RB, (L+1) RB), RB = SMAX 4 NSG; subgroup sid holds rows L RB + s 4 NSG
+// + sid, s < SMAX: p and r in registers, Hp and S in LDS (kkbox's song-id
+// rows: 100 k rows x 2 x 128 B = 25.6 MB of the chip's 40 MB of LDS), q_i
+// read each step (the blocks of an XCD own contiguous rows, so an XCD's q
+// rows stay in its L2).  The state is loaded once after the gradient (R = P = -g,
+// S = 0) and written back when the solve stops or the grid gives up on a
+// barrier (then at step `it`: the state the per-step path continues from,
+// solver.hip cgp_recover).  Per step the arithmetic is k_hs_side_row FUSE's
+// and col_finalize MODE 1's, expression for expression; only the grouping of
+// the grid's dot products differs.
+template <typename real, int KP, int SMAX>
+__global__ __launch_bounds__(BLOCK, sizeof(real) * SMAX <= 16 ? 4 : 2) void k_cg_side_id(uint64_t R, const uint32_t *__restrict__ xidx,
+                                                         const real *__restrict__ xval,
+                                                         const int64_t *__restrict__ cnt, const real *__restrict__ Q1,
+                                                         double w, double n1, Fin<real> f, unsigned *__restrict__ gen,
+                                                         unsigned gen0, int *__restrict__ err_host,
+                                                         int *__restrict__ abort_dev, unsigned spin_max,
+                                                         int stall_step) {
+  using Gm = Geo<real, KP>;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int sg = lane / Gm::LPR, li = lane % Gm::LPR;
+  const unsigned L = (gridDim.x & 7u) ? blockIdx.x : xcd_work_item(blockIdx.x, gridDim.x);
+  const uint64_t base = (uint64_t)L * SMAX * 4 * Gm::NSG + (uint64_t)(wv * Gm::NSG + sg);
+  CgState *st = f.st;
+  __shared__ vec_t<real> Sl[SMAX][BLOCK], Hl[SMAX][BLOCK];
+  vec_t<real> p[SMAX], r[SMAX];
+  real x[SMAX], dd[SMAX], reg[SMAX];
+  uint32_t col[SMAX];
+  const uint64_t nval = R > base ? (R - base + 4 * Gm::NSG - 1) / (4 * Gm::NSG) : 0;  // valid slots: s < nval
+#pragma unroll
+  for (int s = 0; s < SMAX; s++) {
+    const uint64_t i = base + (uint64_t)s * 4 * Gm::NSG;
+    const uint64_t ic = (uint64_t)s < nval ? i : 0;
+    col[s] = xidx[ic];
+    const size_t off = (size_t)col[s] * KP + li * Gm::VE;
+    x[s] = xval[ic];
+    dd[s] = (real)((1 - w) * (double)(cnt[ic + 1] - cnt[ic]) + w * n1);
+    reg[s] = (real)(f.fw ? f.lam * (double)f.fw[col[s]] : f.lam);
+    p[s] = vld<real>(f.P + off);
+    r[s] = vld<real>(f.R + off);
+    Sl[s][threadIdx.x] = vld<real>(f.S + off);
+    Hl[s][threadIdx.x] = vzero<real>();
+  }
+  int done = 0;  // steps computed
+  for (int it = 1; it <= MAXCG; it++) {
+    if (!ald(&st->run[it])) break;  // the same word for every block (read after the barrier)
+    const bool upd = it > 1;
+    const real alpha = upd ? (real)ald(&st->alpha) : (real)0, beta = upd ? (real)ald(&st->beta) : (real)0;
+    if (it == stall_step && blockIdx.x == gridDim.x - 1 && gridDim.x > 1)
+      for (int u = 0; u < 4000; u++) __builtin_amdgcn_s_sleep(127);
+    double dsum[3] = {0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < SMAX; s++) {
+      if ((uint64_t)s >= nval) continue;
+      uint64_t qrow = base + (uint64_t)s * 4 * Gm::NSG;
+      asm volatile("" : "+v"(qrow));  // (the address is recomputed each step, not held)
+      const vec_t<real> q = vld<real>(Q1 + qrow * KP + li * Gm::VE);
+      const vec_t<real> hpo = Hl[s][threadIdx.x];
+      vec_t<real> pt = p[s];
+      if (upd) pt = (r[s] - vsplat<real>(alpha) * hpo) + vsplat<real>(beta) * p[s];
+      const real z = sg_sum<Gm::LPR>(hsum<real>(vsplat<real>(x[s]) * pt * q));
+      const vec_t<real> sum = vsplat<real>(x[s]) * (vsplat<real>(dd[s] * z) * q);
+      // col_finalize MODE 1
+      vec_t<real> rn = r[s], pe = p[s];
+      if (upd) {
+        rn = r[s] - vsplat<real>(alpha) * hpo;
+        pe = rn + vsplat<real>(beta) * p[s];
+        Sl[s][threadIdx.x] = Sl[s][threadIdx.x] + vsplat<real>(alpha) * p[s];
+        r[s] = rn;
+        p[s] = pe;
+      }
+      const vec_t<real> hpn = vsplat<real>(reg[s]) * pe + sum;
+      Hl[s][threadIdx.x] = hpn;
+#pragma unroll
+      for (int e = 0; e < Gm::VE; e++) {
+        dsum[0] += (double)pe[e] * (double)hpn[e];
+        dsum[1] += (double)rn[e] * (double)hpn[e];
+        dsum[2] += (double)hpn[e] * (double)hpn[e];
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one slot at a time (the slots' temporaries are not live together)
+    }
+    done = it;
+    if (!cgp_step_end<real>(f, dsum, it, gen, gen0, err_host, abort_dev, spin_max)) break;
+  }
+  // the state back where the per-step path and the update read it
+  if (done == 0) return;
+#pragma unroll
+  for (int s = 0; s < SMAX; s++) {
+    if ((uint64_t)s >= nval) continue;
+    uint32_t c = col[s];
+    asm volatile("" : "+v"(c));  // recompute the addresses here (else the prologue's stay live in registers)
+    const size_t off = (size_t)c * KP + li * Gm::VE;
+    vst<real>(f.S + off, Sl[s][threadIdx.x]);
+    vst<real>(f.R + off, r[s]);
+    vst<real>(f.P + off, p[s]);
+    vst<real>(f.Hp + off, Hl[s][threadIdx.x]);
+  }
+}
+
 // Per segment of row i: h[s] = (1-w) sum_{j in seg} <phi_i, q_j> q_j
 // + [first] w phi_i QTQ, phi_i = X_i p  (hs_cross row body, ffm.cpp:715-738;
 // tau = X_i (V QTQ) = phi_i QTQ).  QTQ staged in LDS; phi_i's components
@@ -3159,18 +3345,6 @@ __global__ __launch_bounds__(BLOCK) void k_gram_mfma32(uint64_t Rp, const float 
 // share its B rows in the Infinity Cache.  Partials: part[chunk][c * 4096 +
 // m * 64 + n] and the sums at [C * 4096 ..) (k_reduce_parts, fixed order).
 constexpr int GW64 = 1;  // tables per wave of k_gram_mfma64 (64 accumulators each)
-// XCD-aware block order (round 6).  Workgroups are dealt round-robin over
-// the 8 XCDs (blocks b and b + 8 share one, MI355X guide §Workgroup
-// dispatch), so the ngroups blocks of one row chunk — which all read that
-// chunk's B rows — landed on different XCDs and each XCD's L2 fetched B
-// again (config 5: 105.8 GB fetched per launch against 65.3 GB of tables).
-// With the grid a multiple of 8, work item L = (b % 8) * (grid / 8) + b / 8
-// gives each XCD a contiguous run of work items, so the blocks of a chunk
-// run on one XCD back to back and B is fetched into one L2 once.  Work items
-// past nwork (the padding) exit.
-__device__ __forceinline__ unsigned xcd_work_item(unsigned b, unsigned grid) {
-  return (b & 7u) * (grid >> 3) + (b >> 3);
-}
 static __global__ __launch_bounds__(BLOCK, 3) void k_gram_mfma64(uint64_t Rp, int C, const float *const *__restrict__ A,
                                                        const float *__restrict__ B, const float *__restrict__ wv,
                                                        float *__restrict__ part, uint64_t nout,

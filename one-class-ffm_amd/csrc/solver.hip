@@ -3213,6 +3213,64 @@ template <typename real> class Problem final : public ProblemBase {
     });
     return ok;
   }
+  // Persistent CG of an id-like side half (k_cg_side_id): the CG
+  // vectors of the half's rows in registers for the whole solve.  Where the
+  // fused per-step path would run (fused_rows: one GPU, or replicated rows),
+  // with the plain expanded residual, and where the rows fit the resident
+  // grid at <= 4 rows per subgroup (SMAX): kkbox's song-id (100 k, fp32)
+  // and listener-id (30 k) side halves.
+  int sidep_smax(const HalfCtx &h) {
+    if (!sidep_on_ || !fused_rows(h) || exact_r2(h) || h.own->R == 0 ||
+        h.F->excl)
+      return 0;
+    int smax = 0;
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      using Gm = Geo<real, KP>;
+      const uint64_t R = h.own->R;
+      auto fits = [&](auto sm) {
+        constexpr int SM = decltype(sm)::value;
+        return (R + SM * 4 * Gm::NSG - 1) / (SM * 4 * Gm::NSG) <= resident(k_cg_side_id<real, KP, SM>, 0);
+      };
+      if (fits(std::integral_constant<int, 1>())) smax = 1;
+      else if (fits(std::integral_constant<int, 2>())) smax = 2;
+      else if (fits(std::integral_constant<int, 4>())) smax = 4;
+    });
+    return smax;
+  }
+  bool side_persist(HalfCtx &h, int smax) {
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      using Gm = Geo<real, KP>;
+      Fin<real> fin = make_fin(h, 1);
+      DevSide<real> &own = *h.own;
+      DevField<real> &F = *h.F;
+      if (cgp_gen_ > 0xf0000000u) {  // keep clear of CGP_ABORT
+        HIPCHK(hipMemsetAsync(cgp_gen_buf_.p, 0, sizeof(unsigned), stream_));
+        cgp_gen_ = 1;
+      }
+      const unsigned g0 = cgp_gen_;
+      cgp_gen_ += MAXCG + 1;
+      counters["cgp_launches"]++;
+      counters["cgp_side_launches"]++;
+      const double rs = sizeof(real);
+      const double bytes = (double)own.R * KP * rs * 9 + (double)own.R * (4 + rs + 16);
+      auto go = [&](auto sm) {
+        constexpr int SM = decltype(sm)::value;
+        const unsigned need = (unsigned)((own.R + SM * 4 * Gm::NSG - 1) / (SM * 4 * Gm::NSG));
+        const unsigned res = resident(k_cg_side_id<real, KP, SM>, 0);
+        const unsigned grid = (need + 7) / 8 * 8 <= res ? (need + 7) / 8 * 8 : need;  // XCD-ordered when it fits
+        prof_launch("cg_side", bytes, [&] {
+          launch(k_cg_side_id<real, KP, SM>, grid, BLOCK, 0, own.R, F.xidx.p, F.xval.p, hess_cnt(h), h.Q1, w_,
+                 hess_n1(h), fin, cgp_gen_buf_.p, g0, run_host_dev_ + MAXCG + 3, cgp_abort_.p, cgp_spin_, cgp_stall_);
+        });
+      };
+      if (smax == 1) go(std::integral_constant<int, 1>());
+      else if (smax == 2) go(std::integral_constant<int, 2>());
+      else go(std::integral_constant<int, 4>());
+    });
+    return true;
+  }
   // The persistent grid gave up on a barrier (kernels.hpp k_cg_cgram): every
   // column is at step `ab` (the value in the host word) with that step's
   // scalars and verdict published, and the update queued behind the launch
@@ -3454,12 +3512,14 @@ template <typename real> class Problem final : public ProblemBase {
     hot_grams(h);
     if (io) io_begin(h);
     int it0 = 1;
-    if (cgp_ok(h)) {
+    const bool pcg = cgp_ok(h);
+    const int smax = pcg ? 0 : sidep_smax(h);
+    if (pcg || smax) {
       // the whole CG in one persistent launch, the update queued right
       // behind it (no speculation, no host round trip inside the half); the
       // update returns at entry if the grid gave up on its barrier
       prof_tag_ = 1;
-      const bool launched = cg_persist(h);
+      const bool launched = pcg ? cg_persist(h) : side_persist(h, smax);
       prof_tag_ = 0;
       if (launched) {
         finish_half(h, cgp_abort_.p);
@@ -3759,6 +3819,8 @@ template <typename real> class Problem final : public ProblemBase {
   DevBuf<int> cgp_abort_;  // 1: the last persistent grid gave up (guards its queued update)
   unsigned cgp_gen_ = 1, ncu_ = 256;
   bool cgp_on_ = !std::getenv("OCFFM_CGP") || std::atoi(std::getenv("OCFFM_CGP")) != 0;
+  // OCFFM_SIDEP=0: id-like side halves' CG per step (k_hs_side_row FUSE) instead of k_cg_side_id
+  bool sidep_on_ = !std::getenv("OCFFM_SIDEP") || std::atoi(std::getenv("OCFFM_SIDEP")) != 0;
   // OCFFM_CGP_COOP=1: cooperative launch (the runtime's residency check; +0.27 ms per kkbox epoch)
   bool cgp_coop_ = std::getenv("OCFFM_CGP_COOP") && std::atoi(std::getenv("OCFFM_CGP_COOP")) != 0;
   // tests: a short spin limit and one block stalled at a given step force the give-up

@@ -503,6 +503,7 @@ def test_speculative_update_bit_identical(monkeypatch):
                                  {"OCFFM_HOT": "3"}, {"OCFFM_EXACT_R2": "1"}, {"OCFFM_CCG": "0"}, {"OCFFM_CCG": "2"},
                                  {"OCFFM_CGP": "0"}, {"OCFFM_PGRAM": "2"}, {"OCFFM_PGRAM": "0"},
                                  {"OCFFM_SIDE_REFRESH": "1"}, {"OCFFM_SIDE_REFRESH": "0"}, {"OCFFM_TAU_MFMA": "0"},
+                                 {"OCFFM_SIDEP": "0"}, {"OCFFM_GFOLD": "0"},
                                  {"OCFFM_PGRAM": "2", "OCFFM_CGRAM": "2", "OCFFM_CCG": "2"}])
 def test_execution_variants_fp64(kk_small, monkeypatch, env):
     """Schedule knobs (id-field row fusion, segment length, CG look-ahead)
@@ -537,7 +538,7 @@ def test_persistent_cg_gives_up_and_recovers(kk_small, monkeypatch, stall, coop)
         assert_state(o, g, 1e-9)
     np.testing.assert_array_equal(g.cg_log(), o.cg_log())
     launches, recovered = g.counter("cgp_launches"), g.counter("cgp_recovered")
-    assert launches > 0
+    assert launches > 0 and g.counter("cgp_side_launches") > 0  # column-Gram and id-like side halves
     # every launch whose solve reached step `stall` gave up there
     assert recovered > 0
     assert g.counter("cgp_refused") == 0
@@ -674,20 +675,24 @@ def test_kkbox_full_size_parity_fp32(kk_full):
     assert np.abs(g.cg_log().astype(int) - o.cg_log().astype(int)).max() <= 1
 
 
-def test_kdd12_full_size_parity_fp64():
-    """Config 2 at its own size (500 k users x 50 k ads, k = 16):
+@pytest.mark.parametrize("shape", ["kdd12", "outbrain"])
+def test_full_size_metric_parity_fp64(shape):
+    """Configs 2 and 4 at their own sizes (kdd12 500 k users x
+    50 k ads, k = 16; outbrain one GPU's 250 k-row shard, 10 k ads, k = 64):
     one fp64 epoch against the oracle on 16 threads, then validate() on a
     500-row test split.  Here the reference arithmetic does not reproduce
     itself: across thread counts and cblas_ddot orders its CG counts differ
-    in up to 4 of the 42 halves and its tables by 0.4 relative
-    (fp64_envelope.json "kdd12_full"), so no state parity exists at this
-    size; the bound is 3x the spread of its own validation metrics over
-    those runs (tests/golden/kdd12_full_spread.json, tools/kdd12_spread.py),
-    and the CG logs may differ in at most twice as many halves as two
-    reference runs do (ffm.cpp:852-870, 925-1016)."""
+    (kdd12: in up to 6 of the 42 halves, its tables 0.4 apart,
+    fp64_envelope.json "kdd12_full"; outbrain's k = 64 halves run into the
+    20-step cap), so no state parity exists at these sizes.  The bound is 3x
+    the spread of its own validation metrics over those runs
+    (tests/golden/<shape>_full_spread.json, tools/fullsize_spread.py) plus
+    one hit of one test row at each k, and the CG logs may differ in at most
+    twice as many halves as two reference runs do (ffm.cpp:852-870,
+    925-1016)."""
     spread = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
-                                         "kdd12_full_spread.json")))
-    ds = synth.kdd12(test_rows=500)
+                                         f"{shape}_full_spread.json")))
+    ds = getattr(synth, shape)(test_rows=500)
     o = O.Oracle(ds, threads=ORACLE_THREADS)
     g = ocffm.problem_from_dataset(ds, precision=ocffm.FP64)
     ocffm.srand(1)
@@ -698,12 +703,12 @@ def test_kdd12_full_size_parity_fp64():
     g.one_epoch()
     vo, vg = o.validate(), g.validate()
     assert abs(vg["loss"] - vo["loss"]) <= 3 * spread["loss_range"], (vg["loss"], vo["loss"])
-    # plus one hit of one test row at each k (a range of 0 at k = 40, 80 over six runs)
+    # plus one hit of one test row at each k (a range of 0 at large k over six runs)
     one = 1.0 / (ds.test.m * np.array([5, 10, 20, 40, 80]))
     np.testing.assert_array_less(np.abs(vg["prec"] - vo["prec"]), 3 * np.array(spread["prec_range"]) + one + 1e-12)
     np.testing.assert_array_less(np.abs(vg["ndcg"] - vo["ndcg"]), 3 * np.array(spread["ndcg_range"]) + 1e-12)
     cgo, cgg = o.cg_log(), g.cg_log()
-    assert cgo.shape == cgg.shape and int(np.sum(cgo != cgg)) <= 2 * spread["cg_halves_differ"]
+    assert cgo.shape == cgg.shape and int(np.sum(cgo != cgg)) <= 2 * max(1, spread["cg_halves_differ"])
 
 
 def test_kkbox_full_size_properties():

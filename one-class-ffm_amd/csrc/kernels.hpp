@@ -2173,10 +2173,18 @@ constexpr unsigned CGP_SPIN_MAX = 1u << 22;  // ~0.1 s of s_sleep 1: then the gr
 template <typename real, int KP>
 __global__ __launch_bounds__(BLOCK) void k_cg_cgram(uint64_t D, const real *__restrict__ G, Fin<real> f,
                                                     unsigned *__restrict__ gen, unsigned gen0, int *__restrict__ err_host,
-                                                    int *__restrict__ abort_dev, unsigned spin_max, int stall_step) {
+                                                    int *__restrict__ abort_dev, unsigned spin_max, int stall_step,
+                                                    int xcd_cols) {
   using Gm = Geo<real, KP>;
-  WAVE_SETUP
+  const int lane = threadIdx.x & 63;
   const int sg = lane / Gm::LPR, li = lane % Gm::LPR;
+  // XCD-ordered contiguous column ranges (round 6): the blocks of an XCD own
+  // consecutive columns, so an XCD's share of the Grams (artist: 20 MB over
+  // the 8 L2s) is re-read from its own L2 at every step
+  const unsigned L = (gridDim.x & 7u) ? blockIdx.x : xcd_work_item(blockIdx.x, gridDim.x);
+  const uint64_t cpb = (D + gridDim.x - 1) / gridDim.x;  // columns per block
+  const uint64_t c0 = (uint64_t)L * cpb, c1 = c0 + cpb < D ? c0 + cpb : D;
+  const int sid = (threadIdx.x >> 6) * Gm::NSG + sg;
   CgState *st = f.st;
   __shared__ int s_ok;
   for (int it = 1; it <= MAXCG; it++) {
@@ -2187,7 +2195,9 @@ __global__ __launch_bounds__(BLOCK) void k_cg_cgram(uint64_t D, const real *__re
     if (it == stall_step && blockIdx.x == gridDim.x - 1 && gridDim.x > 1)
       for (int q = 0; q < 4000; q++) __builtin_amdgcn_s_sleep(127);
     double dsum[3] = {0, 0, 0};
-    for (uint64_t c = wave * Gm::NSG + sg; c < D; c += nwaves * Gm::NSG) {
+    const uint64_t cb = xcd_cols ? c0 + sid : (uint64_t)blockIdx.x * (BLOCK / Gm::LPR) + sid;
+    const uint64_t ce = xcd_cols ? c1 : D, cs = xcd_cols ? BLOCK / Gm::LPR : (uint64_t)gridDim.x * (BLOCK / Gm::LPR);
+    for (uint64_t c = cb; c < ce; c += cs) {
       const FinOps<real> ops = fin_load<real, KP, 1>(f, (uint32_t)c, upd, li);
       vec_t<real> pt = ops.w_or_p;
       if (upd) pt = (ops.r - vsplat<real>(alpha) * ops.hp) + vsplat<real>(beta) * ops.w_or_p;

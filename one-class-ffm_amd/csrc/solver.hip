@@ -3167,8 +3167,10 @@ template <typename real> class Problem final : public ProblemBase {
       constexpr int KP = decltype(K)::value;
       using Gm = Geo<real, KP>;
       Fin<real> fin = make_fin(h, 1);
-      // at most one block per CU (co-resident unless other work holds the CUs)
-      const unsigned grid = (unsigned)std::min<uint64_t>((h.D + 4 * Gm::NSG - 1) / (4 * Gm::NSG), ncu_);
+      // at most one block per CU (co-resident unless other work holds the CUs),
+      // whole rounds of the 8 XCDs where that stays within the CUs
+      unsigned grid = (unsigned)std::min<uint64_t>((h.D + 4 * Gm::NSG - 1) / (4 * Gm::NSG), ncu_);
+      if (cgp_xcd_ && (grid + 7) / 8 * 8 <= ncu_) grid = (grid + 7) / 8 * 8;
       if (cgp_gen_ > 0xf0000000u) {  // keep clear of CGP_ABORT
         HIPCHK(hipMemsetAsync(cgp_gen_buf_.p, 0, sizeof(unsigned), stream_));
         cgp_gen_ = 1;
@@ -3180,7 +3182,7 @@ template <typename real> class Problem final : public ProblemBase {
       unsigned *genp = cgp_gen_buf_.p;
       int *errh = run_host_dev_ + MAXCG + 3, *abd = cgp_abort_.p;
       unsigned spin = cgp_spin_;
-      int stall = cgp_stall_;
+      int stall = cgp_stall_, xcdc = cgp_xcd_ ? 1 : 0;
       if (grid > resident(k_cg_cgram<real, KP>, 0)) {  // cannot be resident at once: per-step path
         counters["cgp_refused"]++;
         ok = false;
@@ -3189,12 +3191,12 @@ template <typename real> class Problem final : public ProblemBase {
       counters["cgp_launches"]++;
       prof_launch("cg_cgram", 0.0, [&] {
         if (!cgp_coop_) {
-          launch(k_cg_cgram<real, KP>, grid, BLOCK, 0, D, G, fin, genp, g0, errh, abd, spin, stall);
+          launch(k_cg_cgram<real, KP>, grid, BLOCK, 0, D, G, fin, genp, g0, errh, abd, spin, stall, xcdc);
           return;
         }
         // cooperative: the runtime checks that the grid can be resident at
         // once and refuses it otherwise (then: the per-step path)
-        void *args[] = {&D, (void *)&G, &fin, &genp, &g0, &errh, &abd, &spin, &stall};
+        void *args[] = {&D, (void *)&G, &fin, &genp, &g0, &errh, &abd, &spin, &stall, &xcdc};
         if (arm_first_) HIPCHK(hipEventRecord(arm_a_, stream_));
         const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(k_cg_cgram<real, KP>), dim3(grid),
                                                         dim3(BLOCK), args, 0u, stream_);
@@ -3819,6 +3821,8 @@ template <typename real> class Problem final : public ProblemBase {
   DevBuf<int> cgp_abort_;  // 1: the last persistent grid gave up (guards its queued update)
   unsigned cgp_gen_ = 1, ncu_ = 256;
   bool cgp_on_ = !std::getenv("OCFFM_CGP") || std::atoi(std::getenv("OCFFM_CGP")) != 0;
+  // OCFFM_CGP_XCD=0: k_cg_cgram's columns grid-strided instead of XCD-contiguous ranges
+  bool cgp_xcd_ = !std::getenv("OCFFM_CGP_XCD") || std::atoi(std::getenv("OCFFM_CGP_XCD")) != 0;
   // OCFFM_SIDEP=0: id-like side halves' CG per step (k_hs_side_row FUSE) instead of k_cg_side_id
   bool sidep_on_ = !std::getenv("OCFFM_SIDEP") || std::atoi(std::getenv("OCFFM_SIDEP")) != 0;
   // OCFFM_CGP_COOP=1: cooperative launch (the runtime's residency check; +0.27 ms per kkbox epoch)

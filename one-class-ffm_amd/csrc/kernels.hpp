@@ -1364,6 +1364,22 @@ __global__ __launch_bounds__(BLOCK) void k_seg_ysum(uint64_t nseg, const Seg *__
   }
 }
 
+// Per row: yrow[i] = sum of ysum over row i's segments (one wave per row,
+// lanes striding its segments: the rows of popular items have hundreds),
+// for the fused side half (k_cg_side_id FULL), which then reads one value
+// per row.
+template <typename real>
+__global__ __launch_bounds__(BLOCK) void k_row_ysum(uint64_t R, const uint32_t *__restrict__ segptr,
+                                                    const real *__restrict__ ysum, real *__restrict__ yrow) {
+  WAVE_SETUP
+  for (uint64_t i = wave; i < R; i += nwaves) {
+    real z = 0;
+    for (uint32_t q = segptr[i] + lane; q < segptr[i + 1]; q += 64) z += ysum[q];
+    z = sg_sum<64>(z);
+    if (lane == 0) yrow[i] = z;
+  }
+}
+
 // Per segment: h[s] = zpart * q1_i, zpart = sum_{p in seg} ((1-w) y~ - w (1-r))
 // + [first] w (n1 (a_i - r) + sum(b) + sa_i)   (gd_side row body, ffm.cpp:572-589).
 // ysum non-null: the positive sum comes from k_seg_ysum (no positive pass).
@@ -2135,7 +2151,7 @@ __global__ __launch_bounds__(BLOCK) void k_pg_step(uint64_t D, uint32_t QB, cons
 // step's scalars and verdict BEFORE its swap, so an abort at barrier `it`
 // leaves every column at step `it` with the scalars of step `it` in
 // CgState: exactly the state the two-launch path (k_hv_cgram) continues
-// from at step it+1.  The abort is reported as `it` in the host-mapped
+// from at step it+1.  The abort is reported as it + 1 in the host-mapped
 // word and as 1 in `abort_dev`, which guards the update kernels queued
 // behind this launch (they return at entry); the host then resets both
 // words and the generation word and finishes the solve per step.
@@ -2158,7 +2174,7 @@ constexpr unsigned CGP_ABORT = 0xffffffffu;
 #endif
 __device__ __forceinline__ void cgp_report_abort(int *err_host, int *abort_dev, int it) {
   __hip_atomic_store(abort_dev, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(err_host, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(err_host, it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // step + 1: never 0
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 __device__ __forceinline__ double ald(const double *p) {
@@ -2279,7 +2295,9 @@ __global__ __launch_bounds__(BLOCK) void k_cg_cgram(uint64_t D, const real *__re
 // (cg_publish MODE 1, ffm.cpp:803-809, through agent-scope stores) and
 // releases the grid; the others wait (see the co-residency notes above).
 // Returns false when the grid gave up (every block then leaves).
-template <typename real>
+// MODE 0 (it = 0, a fused gradient): publishes g2 = r2 = |G|^2 and the
+// first verdict as cg_publish MODE 0 does (ffm.cpp:773-780).
+template <typename real, int MODE = 1>
 __device__ __forceinline__ bool cgp_step_end(const Fin<real> &f, const double (&dsum)[3], int it, unsigned *gen,
                                              unsigned gen0, int *err_host, int *abort_dev, unsigned spin_max) {
   __shared__ int s_ok;
@@ -2287,16 +2305,26 @@ __device__ __forceinline__ bool cgp_step_end(const Fin<real> &f, const double (&
   double bv[3] = {block_sum(dsum[0]), block_sum(dsum[1]), block_sum(dsum[2])}, tot[3];
   if (last_block<3, 1>(bv, f.part, f.tick, tot)) {  // (a short read-back round: the caller holds state in registers)
     if (threadIdx.x == 0) {
-      const double r2 = ald(&st->r2), g2 = ald(&st->g2);
-      const double a = r2 / tot[0];
-      const double r2n = r2 - 2 * a * tot[1] + a * a * tot[2];
-      ast(&st->vhv, tot[0]);
-      ast(&st->alpha, a);
-      ast(&st->beta, r2n / r2);
-      ast(&st->r2, r2n);
-      ast(&st->nr_cg, it);
-      const int go = (it < MAXCG && g2 * CG_EPS < r2n) ? 1 : 0;
-      ast(&st->run[it + 1], go);
+      int go;
+      if constexpr (MODE == 0) {
+        ast(&st->g2, tot[0]);
+        ast(&st->r2, tot[0]);
+        ast(&st->nr_cg, 0);
+        for (int q = 0; q <= MAXCG + 1; q++) ast(&st->run[q], 0);
+        go = (tot[0] * CG_EPS < tot[0]) ? 1 : 0;
+        ast(&st->run[1], go);
+      } else {
+        const double r2 = ald(&st->r2), g2 = ald(&st->g2);
+        const double a = r2 / tot[0];
+        const double r2n = r2 - 2 * a * tot[1] + a * a * tot[2];
+        ast(&st->vhv, tot[0]);
+        ast(&st->alpha, a);
+        ast(&st->beta, r2n / r2);
+        ast(&st->r2, r2n);
+        ast(&st->nr_cg, it);
+        go = (it < MAXCG && g2 * CG_EPS < r2n) ? 1 : 0;
+        ast(&st->run[it + 1], go);
+      }
       if (f.run_host)
         __hip_atomic_store(f.run_host + it + 1, go ? RUN_GO : RUN_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2358,14 +2386,34 @@ __device__ __forceinline__ bool cgp_step_end(const Fin<real> &f, const double (&
 // solver.hip cgp_recover).  Per step the arithmetic is k_hs_side_row FUSE's
 // and col_finalize MODE 1's, expression for expression; only the grouping of
 // the grid's dot products differs.
-template <typename real, int KP, int SMAX>
+//
+// FULL (round 6): the whole side half in the launch.  Step 0 is the
+// gradient (k_gd_side_seg with the row's sums (k_row_ysum) + the feature
+// pass's col_finalize MODE 0 for the row's one column: G = lam f W + x z q_i,
+// z = (1-w)(Y_i + n_i a_i) - n_i w (1-r) + w (n1 (a_i - r) + sum(b) + sa_i)),
+// published at the barrier as
+// cg_publish MODE 0 does; after the last step the update
+// (k_update_side_row with apply_owned_row: s = S + a p, W += s, P1_i += x s,
+// a_i += <x s, q_i>, the new sum of a to sh.asum).  A grid that gives up
+// (at step 0 too) writes the state back and skips the update: the host
+// continues per step and runs the update itself.
+template <typename real> struct SideHalf {
+  const real *yrow;        // per row: sum of base + partner bias over its positives (k_row_ysum)
+  real *a1;                // this side's bias (updated)
+  const real *sa1;
+  const double *bsum;      // sum of the partner side's bias (read)
+  double *asum;            // sum of this side's new bias (written)
+  real *P1;
+  double r;
+};
+template <typename real, int KP, int SMAX, bool FULL = false>
 __global__ __launch_bounds__(BLOCK, sizeof(real) * SMAX <= 16 ? 4 : 2) void k_cg_side_id(uint64_t R, const uint32_t *__restrict__ xidx,
                                                          const real *__restrict__ xval,
                                                          const int64_t *__restrict__ cnt, const real *__restrict__ Q1,
                                                          double w, double n1, Fin<real> f, unsigned *__restrict__ gen,
                                                          unsigned gen0, int *__restrict__ err_host,
                                                          int *__restrict__ abort_dev, unsigned spin_max,
-                                                         int stall_step) {
+                                                         int stall_step, SideHalf<real> sh) {
   using Gm = Geo<real, KP>;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int sg = lane / Gm::LPR, li = lane % Gm::LPR;
@@ -2386,13 +2434,41 @@ __global__ __launch_bounds__(BLOCK, sizeof(real) * SMAX <= 16 ? 4 : 2) void k_cg
     x[s] = xval[ic];
     dd[s] = (real)((1 - w) * (double)(cnt[ic + 1] - cnt[ic]) + w * n1);
     reg[s] = (real)(f.fw ? f.lam * (double)f.fw[col[s]] : f.lam);
-    p[s] = vld<real>(f.P + off);
-    r[s] = vld<real>(f.R + off);
-    Sl[s][threadIdx.x] = vld<real>(f.S + off);
+    if constexpr (!FULL) {
+      p[s] = vld<real>(f.P + off);
+      r[s] = vld<real>(f.R + off);
+      Sl[s][threadIdx.x] = vld<real>(f.S + off);
+    }
     Hl[s][threadIdx.x] = vzero<real>();
   }
   int done = 0;  // steps computed
-  for (int it = 1; it <= MAXCG; it++) {
+  bool gave_up = false;
+  if constexpr (FULL) {  // step 0: the gradient
+    const real cpos = (real)(1 - w), cneg = (real)(w * (1 - sh.r));
+    const double bs = *sh.bsum;
+    double dsum[3] = {0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < SMAX; s++) {
+      p[s] = r[s] = vzero<real>();
+      Sl[s][threadIdx.x] = vzero<real>();
+      if ((uint64_t)s >= nval) continue;
+      const uint64_t i = base + (uint64_t)s * 4 * Gm::NSG;
+      const real ai = sh.a1[i], n = (real)(cnt[i + 1] - cnt[i]);
+      const real z = (cpos * (sh.yrow[i] + n * ai) - n * cneg) +
+                     (real)(w * (n1 * ((double)ai - sh.r) + bs + (double)sh.sa1[i]));
+      const size_t off = (size_t)col[s] * KP + li * Gm::VE;
+      const vec_t<real> q = vld<real>(Q1 + i * KP + li * Gm::VE);
+      const vec_t<real> g = vsplat<real>(reg[s]) * vld<real>(f.W + off) + vsplat<real>(x[s]) * (vsplat<real>(z) * q);
+      if (f.G) vst<real>(f.G + off, g);
+      r[s] = p[s] = -g;
+#pragma unroll
+      for (int e = 0; e < Gm::VE; e++) dsum[0] += (double)g[e] * (double)g[e];
+    }
+    if (stall_step == 0 && blockIdx.x == gridDim.x - 1 && gridDim.x > 1)
+      for (int u = 0; u < 4000; u++) __builtin_amdgcn_s_sleep(127);
+    gave_up = !cgp_step_end<real, 0>(f, dsum, 0, gen, gen0, err_host, abort_dev, spin_max);
+  }
+  for (int it = 1; it <= MAXCG && !gave_up; it++) {
     if (!ald(&st->run[it])) break;  // the same word for every block (read after the barrier)
     const bool upd = it > 1;
     const real alpha = upd ? (real)ald(&st->alpha) : (real)0, beta = upd ? (real)ald(&st->beta) : (real)0;
@@ -2430,10 +2506,41 @@ __global__ __launch_bounds__(BLOCK, sizeof(real) * SMAX <= 16 ? 4 : 2) void k_cg
       __builtin_amdgcn_sched_barrier(0);  // one slot at a time (the slots' temporaries are not live together)
     }
     done = it;
-    if (!cgp_step_end<real>(f, dsum, it, gen, gen0, err_host, abort_dev, spin_max)) break;
+    if (!cgp_step_end<real>(f, dsum, it, gen, gen0, err_host, abort_dev, spin_max)) {
+      gave_up = true;
+      break;
+    }
+  }
+  if constexpr (FULL) {
+    if (!gave_up) {  // the update (the final step's S + a p)
+      const real alpha = ald(&st->nr_cg) >= 1 ? (real)ald(&st->alpha) : (real)0;
+      double bsn = 0;
+#pragma unroll
+      for (int s = 0; s < SMAX; s++) {
+        if ((uint64_t)s >= nval) continue;
+        uint32_t c = col[s];
+        asm volatile("" : "+v"(c));
+        const size_t off = (size_t)c * KP + li * Gm::VE;
+        const uint64_t i = base + (uint64_t)s * 4 * Gm::NSG;
+        const vec_t<real> sv = Sl[s][threadIdx.x] + vsplat<real>(alpha) * p[s];
+        vst<real>(const_cast<real *>(f.W) + off, vld<real>(f.W + off) + sv);
+        const vec_t<real> xs = vsplat<real>(x[s]) * sv;
+        vst<real>(sh.P1 + i * KP + li * Gm::VE, vld<real>(sh.P1 + i * KP + li * Gm::VE) + xs);
+        const real gap = sg_sum<Gm::LPR>(hsum<real>(xs * vld<real>(Q1 + i * KP + li * Gm::VE)));
+        if (li == 0) {
+          const real an = sh.a1[i] + gap;
+          sh.a1[i] = an;
+          bsn += (double)an;
+        }
+      }
+      const double bv[1] = {block_sum(bsn)};
+      double tot[1];
+      if (last_block<1>(bv, f.part, f.tick, tot) && threadIdx.x == 0) sh.asum[0] = tot[0];
+      return;
+    }
   }
   // the state back where the per-step path and the update read it
-  if (done == 0) return;
+  if (!FULL && done == 0) return;
 #pragma unroll
   for (int s = 0; s < SMAX; s++) {
     if ((uint64_t)s >= nval) continue;

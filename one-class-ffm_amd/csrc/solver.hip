@@ -481,6 +481,7 @@ template <typename real> class Problem final : public ProblemBase {
     dots_.alloc(4);
     bsum_.alloc(2);
     ysum_.alloc(std::max<uint64_t>(std::max(U_.nseg, V_.nseg), 1));
+    yrow_.alloc(std::max<uint64_t>(std::max(U_.R, V_.R), 1));
     // hot rows (opt-in, DESIGN §7: measured no gain at kkbox shape and a
     // loss at config 5): >= OCFFM_HOT positives, in halves whose last CG
     // count was >= OCFFM_HOT_STEPS (default 0 with OCFFM_HOT set)
@@ -2085,16 +2086,7 @@ template <typename real> class Problem final : public ProblemBase {
                              (double)own.R * KP * rs * 2 + (double)own.R * rs * 2;
         DevField<real> &F = *h.F;
         const Fin<real> fin = make_fin(h, 0);
-        // segment sums of base + partner bias: once per side phase (k_seg_ysum)
-        const int ys = h.user ? 0 : 1;
-        if (ysum_on_ && !ysum_ok_[ys] && own.nseg) {
-          prof_launch("seg_ysum", (double)own.npos * (4 + 2 * rs) + (double)own.nseg * (16 + rs), [&] {
-            launch(k_seg_ysum<real, KP>, grid_for(own.nseg, 4 * Gm::NSG), BLOCK, 0, own.nseg, own.segs.p,
-                   own.ycol.p, (const real *)own.yt.p, (const real *)other.bias.p, (uint64_t)other.R, ysum_.p);
-          });
-          ysum_ok_[ys] = true;
-          ysum_ok_[1 - ys] = false;  // one buffer for both sides: the other side's sums are gone
-        }
+        seg_ysum(h);
         const real *ysum = ysum_on_ ? (const real *)ysum_.p : nullptr;
         prof_launch("gd_side_row", bytes, [&] {
           launch(k_gd_side_seg<real, KP>, mfill(k_gd_side_seg<real, KP>, grid_for(own.nseg, 4 * Gm::NSG)), BLOCK, 0, own.nseg, own.segs.p, own.ycol.p,
@@ -2104,6 +2096,40 @@ template <typename real> class Problem final : public ProblemBase {
       }
       feature_pass(h, 0, true);
     });
+  }
+
+  // segment sums of base + partner bias of a side half's rows: once per
+  // side phase (k_seg_ysum)
+  // rows: also the per-row totals (k_row_ysum, the fused side half's input)
+  void seg_ysum(const HalfCtx &h, bool rows = false) {
+    DevSide<real> &own = *h.own, &other = h.user ? V_ : U_;
+    const int ys = h.user ? 0 : 1;
+    if (!ysum_on_ || !own.nseg) return;
+    if (ysum_ok_[ys]) {
+      if (rows && !yrow_ok_[ys]) row_ysum(own, ys);
+      return;
+    }
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      using Gm = Geo<real, KP>;
+      const double rs = sizeof(real);
+      prof_launch("seg_ysum", (double)own.npos * (4 + 2 * rs) + (double)own.nseg * (16 + rs), [&] {
+        launch(k_seg_ysum<real, KP>, grid_for(own.nseg, 4 * Gm::NSG), BLOCK, 0, own.nseg, own.segs.p, own.ycol.p,
+               (const real *)own.yt.p, (const real *)other.bias.p, (uint64_t)other.R, ysum_.p);
+      });
+    });
+    ysum_ok_[ys] = true;
+    ysum_ok_[1 - ys] = false;  // one buffer for both sides: the other side's sums are gone
+    yrow_ok_[0] = yrow_ok_[1] = false;
+    if (rows) row_ysum(own, ys);
+  }
+  void row_ysum(DevSide<real> &own, int ys) {
+    prof_launch("row_ysum", (double)own.R * 8 + (double)own.nseg * sizeof(real) + (double)own.R * sizeof(real), [&] {
+      launch(k_row_ysum<real>, grid_for(own.R, BLOCK / 64, 8192), BLOCK, 0, (uint64_t)own.R, (const uint32_t *)own.segptr.p,
+             (const real *)ysum_.p, yrow_.p);
+    });
+    yrow_ok_[ys] = true;
+    yrow_ok_[1 - ys] = false;
   }
 
   // subgroups per wave of this problem's row geometry (kernels.hpp: Geo)
@@ -3221,9 +3247,14 @@ template <typename real> class Problem final : public ProblemBase {
   // with the plain expanded residual, and where the rows fit the resident
   // grid at <= 4 rows per subgroup (SMAX): kkbox's song-id (100 k, fp32)
   // and listener-id (30 k) side halves.
-  int sidep_smax(const HalfCtx &h) {
+  // full: the whole half in the launch (k_cg_side_id FULL: gradient, CG
+  // and update), where the gradient reads the segment sums and nothing
+  // else runs between the gradient and the CG (one GPU; no Gram path).
+  int sidep_smax(const HalfCtx &h, bool full = false) {
     if (!sidep_on_ || !fused_rows(h) || exact_r2(h) || h.own->R == 0 ||
         h.F->excl)
+      return 0;
+    if (full && (!sidef_on_ || comm_.active() || !ysum_on_ || !h.own->nseg || pgram(h) || cgram(h) || hot(h)))
       return 0;
     int smax = 0;
     with_kp(kp_, [&](auto K) {
@@ -3232,7 +3263,8 @@ template <typename real> class Problem final : public ProblemBase {
       const uint64_t R = h.own->R;
       auto fits = [&](auto sm) {
         constexpr int SM = decltype(sm)::value;
-        return (R + SM * 4 * Gm::NSG - 1) / (SM * 4 * Gm::NSG) <= resident(k_cg_side_id<real, KP, SM>, 0);
+        const unsigned res = full ? resident(k_cg_side_id<real, KP, SM, true>, 0) : resident(k_cg_side_id<real, KP, SM>, 0);
+        return (R + SM * 4 * Gm::NSG - 1) / (SM * 4 * Gm::NSG) <= res;
       };
       if (fits(std::integral_constant<int, 1>())) smax = 1;
       else if (fits(std::integral_constant<int, 2>())) smax = 2;
@@ -3240,11 +3272,15 @@ template <typename real> class Problem final : public ProblemBase {
     });
     return smax;
   }
-  bool side_persist(HalfCtx &h, int smax) {
+  bool side_persist(HalfCtx &h, int smax, bool full = false) {
+    if (full) {
+      flush_base();  // (gradient's work ahead of the gradient pass)
+      seg_ysum(h, true);
+    }
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
       using Gm = Geo<real, KP>;
-      Fin<real> fin = make_fin(h, 1);
+      Fin<real> fin = make_fin(h, full ? 0 : 1);
       DevSide<real> &own = *h.own;
       DevField<real> &F = *h.F;
       if (cgp_gen_ > 0xf0000000u) {  // keep clear of CGP_ABORT
@@ -3255,17 +3291,28 @@ template <typename real> class Problem final : public ProblemBase {
       cgp_gen_ += MAXCG + 1;
       counters["cgp_launches"]++;
       counters["cgp_side_launches"]++;
+      if (full) counters["cgp_side_full"]++;
       const double rs = sizeof(real);
       const double bytes = (double)own.R * KP * rs * 9 + (double)own.R * (4 + rs + 16);
+      DevSide<real> &other = h.user ? V_ : U_;
+      SideHalf<real> sh{(const real *)yrow_.p, own.bias.p, own.s.p,
+                        bsum_.p + (h.user ? 1 : 0), bsum_.p + (h.user ? 0 : 1), h.P1, r_};
+      (void)other;
       auto go = [&](auto sm) {
         constexpr int SM = decltype(sm)::value;
-        const unsigned need = (unsigned)((own.R + SM * 4 * Gm::NSG - 1) / (SM * 4 * Gm::NSG));
-        const unsigned res = resident(k_cg_side_id<real, KP, SM>, 0);
-        const unsigned grid = (need + 7) / 8 * 8 <= res ? (need + 7) / 8 * 8 : need;  // XCD-ordered when it fits
-        prof_launch("cg_side", bytes, [&] {
-          launch(k_cg_side_id<real, KP, SM>, grid, BLOCK, 0, own.R, F.xidx.p, F.xval.p, hess_cnt(h), h.Q1, w_,
-                 hess_n1(h), fin, cgp_gen_buf_.p, g0, run_host_dev_ + MAXCG + 3, cgp_abort_.p, cgp_spin_, cgp_stall_);
-        });
+        auto kern = [&](auto fl) {
+          constexpr bool FL = decltype(fl)::value;
+          const unsigned need = (unsigned)((own.R + SM * 4 * Gm::NSG - 1) / (SM * 4 * Gm::NSG));
+          const unsigned res = resident(k_cg_side_id<real, KP, SM, FL>, 0);
+          const unsigned grid = (need + 7) / 8 * 8 <= res ? (need + 7) / 8 * 8 : need;  // XCD-ordered when it fits
+          prof_launch(FL ? "side_half" : "cg_side", bytes, [&] {
+            launch(k_cg_side_id<real, KP, SM, FL>, grid, BLOCK, 0, own.R, F.xidx.p, F.xval.p, hess_cnt(h), h.Q1, w_,
+                   hess_n1(h), fin, cgp_gen_buf_.p, g0, run_host_dev_ + MAXCG + 3, cgp_abort_.p, cgp_spin_,
+                   cgp_stall_, sh);
+          });
+        };
+        if (full) kern(std::true_type());
+        else kern(std::false_type());
       };
       if (smax == 1) go(std::integral_constant<int, 1>());
       else if (smax == 2) go(std::integral_constant<int, 2>());
@@ -3274,15 +3321,16 @@ template <typename real> class Problem final : public ProblemBase {
     return true;
   }
   // The persistent grid gave up on a barrier (kernels.hpp k_cg_cgram): every
-  // column is at step `ab` (the value in the host word) with that step's
+  // column is at step `ab` (the host word holds ab + 1; ab = 0: the fused
+  // side half gave up after its gradient, k_side_id_half) with that step's
   // scalars and verdict published, and the update queued behind the launch
   // returned at entry.  Reset the abort words and the generation word, read
   // the verdicts up to ab + 1, and return the step the per-step loop
   // continues with.
   template <class Ex> int cgp_recover(Ex &examine, bool &gave_up, bool &queued) {
     HIPCHK(hipStreamSynchronize(stream_));
-    const int ab = __atomic_load_n(&run_host_[MAXCG + 3], __ATOMIC_ACQUIRE);
-    if (ab < 1 || ab > MAXCG) throw Error(OCFFM_E_STATE, "persistent CG: bad abort step " + std::to_string(ab));
+    const int ab = __atomic_load_n(&run_host_[MAXCG + 3], __ATOMIC_ACQUIRE) - 1;  // the word holds step + 1
+    if (ab < 0 || ab > MAXCG) throw Error(OCFFM_E_STATE, "persistent CG: bad abort step " + std::to_string(ab));
     run_host_[MAXCG + 3] = 0;
     std::atomic_thread_fence(std::memory_order_seq_cst);
     HIPCHK(hipMemsetAsync(cgp_abort_.p, 0, sizeof(int), stream_));
@@ -3509,13 +3557,35 @@ template <typename real> class Problem final : public ProblemBase {
     const int last = key < pred_.size() ? pred_[key] : 0;
     ccg_now_ = ccg_eligible(h) && (ccg_mode_ == 2 || last >= 3);
     hot_now_ = last >= hot_steps_;
-    gradient(h);
-    col_grams(h);
-    hot_grams(h);
-    if (io) io_begin(h);
     int it0 = 1;
-    const bool pcg = cgp_ok(h);
-    const int smax = pcg ? 0 : sidep_smax(h);
+    const int sfull = sidep_smax(h, true);
+    if (sfull) {
+      // the whole half in one launch (k_cg_side_id FULL): gradient, CG and
+      // update; if the grid gave up (at the gradient's barrier too) the
+      // host continues per step from the state it wrote back, and updates
+      prof_tag_ = 1;
+      side_persist(h, sfull, true);
+      prof_tag_ = 0;
+      ysum_ok_[h.user ? 1 : 0] = false;  // (the update moves this side's bias: finish_half's bookkeeping)
+      examine(MAXCG);
+      queued = true;
+      if (gave_up) it0 = cgp_recover(examine, gave_up, queued);
+      if (profiling && pending_.size() > pend0) {  // its bytes: the gradient, the steps and the update that ran
+        const double rs = sizeof(real), k = (double)kp_, R = (double)h.own->R;
+        const int steps = it0 > 1 ? it0 - 1 : nr;
+        for (size_t q = pend0; q < pending_.size(); q++)
+          if (pending_[q].name == "side_half")
+            pending_[q].bytes = R * (8 + 4 + rs + 16 + 3 * rs) + (double)h.own->nseg * (16 + rs) +
+                                (double)h.D * k * rs * 3 + 2 * R * k * rs + (steps + 2) * R * k * rs;
+      }
+    } else {
+      gradient(h);
+      col_grams(h);
+      hot_grams(h);
+      if (io) io_begin(h);
+    }
+    const bool pcg = !sfull && cgp_ok(h);
+    const int smax = pcg || sfull ? 0 : sidep_smax(h);
     if (pcg || smax) {
       // the whole CG in one persistent launch, the update queued right
       // behind it (no speculation, no host round trip inside the half); the
@@ -3696,6 +3766,8 @@ template <typename real> class Problem final : public ProblemBase {
   // the expanded scalar of the finalisation (OCFFM_EXACT_R2=1)
   bool exact_r2_ = std::getenv("OCFFM_EXACT_R2") && std::atoi(std::getenv("OCFFM_EXACT_R2")) != 0;
   bool ysum_ok_[2] = {false, false};
+  DevBuf<real> yrow_;                 // per-row totals of the segment sums (k_row_ysum)
+  bool yrow_ok_[2] = {false, false};  // (valid only with ysum_ok_ of the side)
   // Cross loop: the item halves read the block-excluded value through perm
   // from the user orientation (k_gd_cross_seg ytv) instead of a refresh after
   // each entering pass.  OCFFM_YTVIA=0: refresh.
@@ -3825,11 +3897,13 @@ template <typename real> class Problem final : public ProblemBase {
   bool cgp_xcd_ = !std::getenv("OCFFM_CGP_XCD") || std::atoi(std::getenv("OCFFM_CGP_XCD")) != 0;
   // OCFFM_SIDEP=0: id-like side halves' CG per step (k_hs_side_row FUSE) instead of k_cg_side_id
   bool sidep_on_ = !std::getenv("OCFFM_SIDEP") || std::atoi(std::getenv("OCFFM_SIDEP")) != 0;
+  // OCFFM_SIDE_FULL=0: id-like side halves run gradient and update as their own launches around k_cg_side_id
+  bool sidef_on_ = !std::getenv("OCFFM_SIDE_FULL") || std::atoi(std::getenv("OCFFM_SIDE_FULL")) != 0;
   // OCFFM_CGP_COOP=1: cooperative launch (the runtime's residency check; +0.27 ms per kkbox epoch)
   bool cgp_coop_ = std::getenv("OCFFM_CGP_COOP") && std::atoi(std::getenv("OCFFM_CGP_COOP")) != 0;
   // tests: a short spin limit and one block stalled at a given step force the give-up
   unsigned cgp_spin_ = std::getenv("OCFFM_CGP_SPIN") ? (unsigned)std::atol(std::getenv("OCFFM_CGP_SPIN")) : CGP_SPIN_MAX;
-  int cgp_stall_ = std::getenv("OCFFM_CGP_STALL") ? std::atoi(std::getenv("OCFFM_CGP_STALL")) : 0;
+  int cgp_stall_ = std::getenv("OCFFM_CGP_STALL") ? std::atoi(std::getenv("OCFFM_CGP_STALL")) : -1;
   real *stage_ = nullptr;
   static constexpr uint64_t DSTAGE = 64;
   double *dstage_ = nullptr;  // host all-reduce stage of the owned-field dot products

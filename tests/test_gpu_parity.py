@@ -503,7 +503,7 @@ def test_speculative_update_bit_identical(monkeypatch):
                                  {"OCFFM_HOT": "3"}, {"OCFFM_EXACT_R2": "1"}, {"OCFFM_CCG": "0"}, {"OCFFM_CCG": "2"},
                                  {"OCFFM_CGP": "0"}, {"OCFFM_PGRAM": "2"}, {"OCFFM_PGRAM": "0"},
                                  {"OCFFM_SIDE_REFRESH": "1"}, {"OCFFM_SIDE_REFRESH": "0"}, {"OCFFM_TAU_MFMA": "0"},
-                                 {"OCFFM_SIDEP": "0"}, {"OCFFM_GFOLD": "0"},
+                                 {"OCFFM_SIDEP": "0"}, {"OCFFM_GFOLD": "0"}, {"OCFFM_SIDE_FULL": "0"},
                                  {"OCFFM_PGRAM": "2", "OCFFM_CGRAM": "2", "OCFFM_CCG": "2"}])
 def test_execution_variants_fp64(kk_small, monkeypatch, env):
     """Schedule knobs (id-field row fusion, segment length, CG look-ahead)
@@ -518,14 +518,16 @@ def test_execution_variants_fp64(kk_small, monkeypatch, env):
 
 
 @pytest.mark.parametrize("coop", ["1", "0"])
-@pytest.mark.parametrize("stall", ["1", "2", "3"])
+@pytest.mark.parametrize("stall", ["0", "1", "2", "3"])
 def test_persistent_cg_gives_up_and_recovers(kk_small, monkeypatch, stall, coop):
     """The persistent column-Gram CG (k_cg_cgram) forced to give up on its
     grid barrier: one block sleeps before step `stall` while the others'
     spin limit is tiny, as when other processes hold CUs.  The grid stops at
     that step with the state consistent, the update queued behind it returns
     at entry, and the host finishes the solve per step (solver.hip
-    cgp_recover).  Two epochs (the second starts from recovered state:
+    cgp_recover).  The fused id-like side halves (k_cg_side_id FULL) give up
+    the same way; stall 0 is their gradient's barrier (the host then runs
+    the whole CG and the update).  Two epochs (the second starts from recovered state:
     tickets, generation word, abort words) within 1e-9 of the oracle with
     identical CG counts (ffm.cpp:761-812)."""
     monkeypatch.setenv("OCFFM_CGP_SPIN", "2000")
@@ -539,6 +541,7 @@ def test_persistent_cg_gives_up_and_recovers(kk_small, monkeypatch, stall, coop)
     np.testing.assert_array_equal(g.cg_log(), o.cg_log())
     launches, recovered = g.counter("cgp_launches"), g.counter("cgp_recovered")
     assert launches > 0 and g.counter("cgp_side_launches") > 0  # column-Gram and id-like side halves
+    assert g.counter("cgp_side_full") > 0
     # every launch whose solve reached step `stall` gave up there
     assert recovered > 0
     assert g.counter("cgp_refused") == 0

@@ -2554,6 +2554,98 @@ __global__ __launch_bounds__(BLOCK, sizeof(real) * SMAX <= 16 ? 4 : 2) void k_cg
   }
 }
 
+// Cross Hessian-vector product of an id-like field, fused with its
+// finalisation (round 6; one GPU): row i is column c = xidx[i]'s only row,
+// so the feature pass of hs_cross (ffm.cpp:715-742, then 783-809) reduces
+// to the row itself, as k_hs_side_row FUSE does for side halves:
+//   Hp_c = lam f pt_c + x_i ((1-w) sum_{j in pos(i)} <phi, q_j> q_j + w phi QTQ),
+//   phi = x_i pt_c,
+// one launch per CG step instead of k_hs_cross_seg + k_feat.  The gathers
+// are k_hs_cross_seg's over the row's positives; the tau term takes QTQ
+// from LDS (k_feat TAU's per-column form); a hot row (hot_row[i] !=
+// HOT_NONE: more positives than one gather pass) reads its Gram
+// G_i = sum_j q_j q_j^T (k_hot_gram, built for the half), so no subgroup
+// walks a popular item's thousands of positives.
+template <typename real, int KP> constexpr bool xfuse_kp() { return KP <= 64; }  // (QTQ in LDS)
+// XGB: gathers per round (8: 4 waves per SIMD at <= 128 registers; 16:
+// the compiler's choice, ~166 registers)
+template <typename real, int KP, int XGB = 8>
+__global__ __launch_bounds__(BLOCK, XGB >= 16 ? 1 : 4) void k_hv_cross_id(
+    uint64_t R, const uint32_t *__restrict__ xidx, const real *__restrict__ xval, const int64_t *__restrict__ yptr,
+    const uint32_t *__restrict__ ycol, const real *__restrict__ Q1, uint64_t q1rows, const real *__restrict__ QTQ,
+    double w, const uint32_t *__restrict__ hot_row, const real *__restrict__ hotG, Fin<real> f) {
+  using G = Geo<real, KP>;
+  using PP = PosPass<real, KP, sizeof(real) == 8 ? XGB / 2 : XGB, 32>;
+  if constexpr (!xfuse_kp<real, KP>()) return;
+  if (!f.st->run[f.it]) return;
+  const BufView qb = buf_view(Q1, q1rows * KP * sizeof(real));
+  __shared__ __align__(16) real Qs[xfuse_kp<real, KP>() ? KP * KP : 1];
+  for (int t = threadIdx.x; t < KP * KP; t += BLOCK) Qs[t] = QTQ[t];
+  __syncthreads();
+  const bool upd = f.it > 1;
+  const real alpha = upd ? (real)f.st->alpha : (real)0, beta = upd ? (real)f.st->beta : (real)0;
+  const real cpos = (real)(1 - w), wr = (real)w;
+  WAVE_SETUP
+  const int sg = lane / G::LPR, li = lane % G::LPR;
+  double dsum[3] = {0, 0, 0};
+  for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
+    const uint32_t c = xidx[i];
+    const real x = xval[i];
+    const int64_t b = yptr[i], e = yptr[i + 1];
+    const uint32_t hs = hot_row ? hot_row[i] : HOT_NONE;
+    uint32_t jj[PP::UT];  // the first pass's columns go out with the finalisation operands
+    if (hs == HOT_NONE) PP::load_cols(ycol, b, e, li, jj);
+    // col_finalize MODE 1's update part first (it does not depend on the
+    // product): S += a p, r -= a Hp, p = r + b p; then only p (= pt) and r
+    // stay live across the gathers
+    const size_t off = (size_t)c * KP + li * G::VE;
+    const real reg = (real)(f.fw ? f.lam * (double)f.fw[c] : f.lam);
+    vec_t<real> pt = vld<real>(f.P + off), rn = vld<real>(f.R + off);
+    if (upd) {
+      const vec_t<real> hp = vld<real>(f.Hp + off), so = vld<real>(f.S + off);
+      vst<real>(f.S + off, so + vsplat<real>(alpha) * pt);
+      rn = rn - vsplat<real>(alpha) * hp;
+      pt = rn + vsplat<real>(beta) * pt;
+      vst<real>(f.R + off, rn);
+      vst<real>(f.P + off, pt);
+    }
+    const vec_t<real> phi = vsplat<real>(x) * pt;
+    vec_t<real> ka = vzero<real>();
+    if (hs != HOT_NONE) {
+      ka = sg_vecmat_rolled<real, KP>(phi, hotG + (size_t)hs * KP * KP, li);
+    } else {
+      for (int64_t p0 = b; p0 < e; p0 += PP::PW) {
+        if (p0 != b) PP::load_cols(ycol, p0, e, li, jj);
+        sfor<PP::PW / PP::GB>([&](auto BT) {
+          constexpr int bt = decltype(BT)::value * PP::GB;
+          if (p0 + bt >= e) return;
+          vec_t<real> qv[PP::GB];
+          sfor<PP::GB>([&](auto U) {
+            constexpr int u = decltype(U)::value;
+            qv[u] = bld<real>(qb, PP::row_off(PP::template at<bt + u>(jj, li), qb, li));
+          });
+          real dv[PP::GB];
+#pragma unroll
+          for (int u = 0; u < PP::GB; u++) dv[u] = sg_sum<G::LPR>(hsum<real>(phi * qv[u]));
+#pragma unroll
+          for (int u = 0; u < PP::GB; u++) ka += vsplat<real>(dv[u]) * qv[u];
+        });
+      }
+    }
+    const vec_t<real> s =
+        vsplat<real>(x) * (vsplat<real>(cpos) * ka + vsplat<real>(wr) * sg_vecmat_rolled<real, KP, 2>(phi, Qs, li));
+    const vec_t<real> hp = vsplat<real>(reg) * pt + s;
+    vst<real>(f.Hp + off, hp);
+#pragma unroll
+    for (int q = 0; q < G::VE; q++) {
+      dsum[0] += (double)pt[q] * (double)hp[q];
+      dsum[1] += (double)rn[q] * (double)hp[q];
+      dsum[2] += (double)hp[q] * (double)hp[q];
+    }
+  }
+  fin_blocks<real, 1>(f, dsum);
+}
+
 // Per segment of row i: h[s] = (1-w) sum_{j in seg} <phi_i, q_j> q_j
 // + [first] w phi_i QTQ, phi_i = X_i p  (hs_cross row body, ffm.cpp:715-738;
 // tau = X_i (V QTQ) = phi_i QTQ).  QTQ staged in LDS; phi_i's components

@@ -203,6 +203,8 @@ template <typename real> struct DevSide {
   // (built once per cross half) instead of gathering them every CG step.
   uint64_t nhot = 0, hslots = 0, hpos = 0;  // rows, partial slots, their positives
   DevBuf<uint32_t> hot_seg;                  // per segment: the row's Gram slot or HOT_NONE
+  DevBuf<uint32_t> hot_row;                  // per row: its Gram slot or HOT_NONE
+  bool xf_ok = false;                        // every row under the hot threshold, or the hot rows' Grams set up
   DevBuf<Job> hchunks, hsums;
 };
 
@@ -488,8 +490,16 @@ template <typename real> class Problem final : public ProblemBase {
     if (const char *e = std::getenv("OCFFM_HOT")) {
       hot_min_ = std::strtoull(e, nullptr, 10);
       hot_steps_ = 0;
+      hot_env_ = hot_min_ > 0;
     }
     if (const char *e = std::getenv("OCFFM_HOT_STEPS")) hot_steps_ = std::atoi(e);
+    // the fused cross steps of id-like fields (k_hv_cross_id) read the Grams
+    // of rows with >= OCFFM_XF_HOT positives (default: more than one gather
+    // pass, 33) instead of gathering them
+    if (!hot_env_ && xfuse_on_ && !comm_.active()) {
+      const char *e = std::getenv("OCFFM_XF_HOT");
+      hot_min_ = e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : 33;
+    }
     if (C_ > 0 && hot_min_ > 0) {
       hot_setup(U_);
       hot_setup(V_);
@@ -2236,6 +2246,7 @@ template <typename real> class Problem final : public ProblemBase {
     std::vector<uint32_t> row_slot(s.R, HOT_NONE);
     std::vector<std::pair<uint64_t, uint64_t>> ranges;
     uint64_t nhot = 0, slots = 0, hpos = 0;
+    s.xf_ok = false;
     for (uint64_t i = 0; i < s.R; i++) {
       const uint64_t b = (uint64_t)yp[i], e = (uint64_t)yp[i + 1];
       if (e - b < hot_min_) continue;
@@ -2244,7 +2255,10 @@ template <typename real> class Problem final : public ProblemBase {
       hpos += e - b;
       nhot++;
     }
+    s.xf_ok = nhot == 0;
     if (!nhot) return;
+    if (!hot_env_ && 2 * hpos > s.npos) return;  // (k_hv_cross_id's gate: the Grams would replace most gathers)
+    s.xf_ok = true;
     std::vector<Job> chunks, sums;
     gram_chunks(ranges, chunks, sums, slots);
     s.nhot = nhot;
@@ -2254,6 +2268,7 @@ template <typename real> class Problem final : public ProblemBase {
     s.hsums.upload(sums);
     DevBuf<uint32_t> rs;
     rs.upload(row_slot);
+    s.hot_row.upload(row_slot);
     s.hot_seg.alloc(s.nseg);
     launch(k_hot_seg, (unsigned)((s.nseg + BLOCK - 1) / BLOCK), BLOCK, 0, (uint64_t)s.nseg, (const Seg *)s.segs.p,
            (const uint32_t *)rs.p, s.hot_seg.p);
@@ -2262,12 +2277,14 @@ template <typename real> class Problem final : public ProblemBase {
   // A cross half reads hot rows' Grams when its previous CG count was at
   // least hot_steps_ (the build is one MFMA pass over the hot positives;
   // each step then saves their gathers) and it is not on column Grams.
-  bool hot(const HalfCtx &h) const { return hot_now_ && h.cross && h.own->nhot > 0 && hotG_.p && !ccg_now_; }
+  bool hot(const HalfCtx &h) const {
+    return hot_env_ && hot_now_ && h.cross && h.own->nhot > 0 && hotG_.p && !ccg_now_;
+  }
 
   // The hot rows' Grams G_i = sum_{j in Omega_i} q_j q_j^T over this half's
   // partner table (fixed over the half's CG steps).
-  void hot_grams(const HalfCtx &h) {
-    if (!hot(h)) return;
+  void hot_grams(const HalfCtx &h, bool force = false) {
+    if (!(force ? h.own->nhot > 0 && hotG_.p : hot(h))) return;
     DevSide<real> &own = *h.own;
     with_kp(kp_, [&](auto K) {
       constexpr int KP = decltype(K)::value;
@@ -3386,11 +3403,51 @@ template <typename real> class Problem final : public ProblemBase {
     sd.short_segs = (double)small >= 0.99 * (double)sd.nseg;
   }
 
+  // Fused cross steps (k_hv_cross_id): an id-like cross half on one GPU
+  // whose hot rows (Grams) hold a minority of the positives.
+  bool xfuse(const HalfCtx &h) const {
+    if (!xfuse_on_ || !h.cross || !h.F->idlike || comm_.active() || h.F->excl || cgram(h) || pgram(h) || ccg_now_ ||
+        hot(h) || h.own->R == 0 || !qtq_ || kp_ > 64 || !h.own->xf_ok)
+      return false;
+    return h.own->nhot == 0 || hotG_.p;
+  }
+  void hv_cross_id(HalfCtx &h, int it) {
+    DevSide<real> &own = *h.own;
+    const bool hotr = own.nhot > 0 && hotG_.p;
+    with_kp(kp_, [&](auto K) {
+      constexpr int KP = decltype(K)::value;
+      if constexpr (xfuse_kp<real, KP>()) {
+        using Gm = Geo<real, KP>;
+        const double rs = sizeof(real);
+        DevField<real> &F = *h.F;
+        const Fin<real> fin = make_fin(h, it);
+        const double bytes = (double)own.R * (16 + 4 + rs + 4) + (double)(own.npos - own.hpos) * (4 + KP * rs) +
+                             (double)own.nhot * KP * KP * rs + (double)h.D * KP * rs * (it > 1 ? 8 : 3);
+        auto go = [&](auto gb) {
+          constexpr int GB = decltype(gb)::value;
+          unsigned grid = grid_for(own.R, 4 * Gm::NSG, hs_blocks_);
+          if (row_fill_) grid = std::min(grid, resident(k_hv_cross_id<real, KP, GB>, 0));
+          launch(k_hv_cross_id<real, KP, GB>, grid, BLOCK, 0, own.R, F.xidx.p, F.xval.p, (const int64_t *)own.yptr.p,
+                 (const uint32_t *)own.ycol.p, h.Q1, (uint64_t)h.partner->R, (const real *)qtq_, w_,
+                 hotr ? (const uint32_t *)own.hot_row.p : (const uint32_t *)nullptr, (const real *)hotG_.p, fin);
+        };
+        prof_launch("hv_cross_id", bytes, [&] {
+          if (xf_gb_ >= 16) go(std::integral_constant<int, 16>());
+          else go(std::integral_constant<int, 8>());
+        });
+      }
+    });
+  }
+
   void hv_product(HalfCtx &h, int it) {
     DevSide<real> &own = *h.own;
     const int *run = &st_.p->run[it];
     if (io_half(h)) {
       hv_io(h, it);
+      return;
+    }
+    if (xfuse(h)) {
+      hv_cross_id(h, it);
       return;
     }
     if (cgram(h)) {
@@ -3581,7 +3638,7 @@ template <typename real> class Problem final : public ProblemBase {
     } else {
       gradient(h);
       col_grams(h);
-      hot_grams(h);
+      hot_grams(h, xfuse(h));
       if (io) io_begin(h);
     }
     const bool pcg = !sfull && cgp_ok(h);
@@ -3811,6 +3868,7 @@ template <typename real> class Problem final : public ProblemBase {
   uint64_t hot_min_ = 0;
   DevBuf<real> hotG_, hotP_;
   int hot_steps_ = 6;
+  bool hot_env_ = false;  // OCFFM_HOT set: the per-step cross passes read hot rows' Grams
   bool hot_now_ = false;
   // default: on where the build runs on MFMA (fp32, KP 32 / 64); the fp64
   // VALU build measured slower than the steps it saves
@@ -3899,6 +3957,9 @@ template <typename real> class Problem final : public ProblemBase {
   bool sidep_on_ = !std::getenv("OCFFM_SIDEP") || std::atoi(std::getenv("OCFFM_SIDEP")) != 0;
   // OCFFM_SIDE_FULL=0: id-like side halves run gradient and update as their own launches around k_cg_side_id
   bool sidef_on_ = !std::getenv("OCFFM_SIDE_FULL") || std::atoi(std::getenv("OCFFM_SIDE_FULL")) != 0;
+  // OCFFM_XFUSE=0: id-like cross halves' CG steps as k_hs_cross_seg + feature pass instead of k_hv_cross_id
+  bool xfuse_on_ = !std::getenv("OCFFM_XFUSE") || std::atoi(std::getenv("OCFFM_XFUSE")) != 0;
+  int xf_gb_ = std::getenv("OCFFM_XF_GB") ? std::atoi(std::getenv("OCFFM_XF_GB")) : 8;  // gathers per round (8 or 16)
   // OCFFM_CGP_COOP=1: cooperative launch (the runtime's residency check; +0.27 ms per kkbox epoch)
   bool cgp_coop_ = std::getenv("OCFFM_CGP_COOP") && std::atoi(std::getenv("OCFFM_CGP_COOP")) != 0;
   // tests: a short spin limit and one block stalled at a given step force the give-up

@@ -2588,11 +2588,25 @@ __global__ __launch_bounds__(BLOCK, XGB >= 16 ? 1 : 4) void k_hv_cross_id(
   WAVE_SETUP
   const int sg = lane / G::LPR, li = lane % G::LPR;
   double dsum[3] = {0, 0, 0};
-  for (uint64_t i = wave * G::NSG + sg; i < R; i += nwaves * G::NSG) {
-    const uint32_t c = xidx[i];
-    const real x = xval[i];
-    const int64_t b = yptr[i], e = yptr[i + 1];
-    const uint32_t hs = hot_row ? hot_row[i] : HOT_NONE;
+  // the next row's descriptor in flight while this one is processed (a
+  // resident grid, OCFFM_ROW_FILL, walks several rows per subgroup)
+  const uint64_t stride = nwaves * G::NSG;
+  uint32_t nc = 0, nh = HOT_NONE;
+  real nx = 0;
+  int64_t nb = 0, ne = 0;
+  auto fetch = [&](uint64_t q) {
+    nc = xidx[q];
+    nx = xval[q];
+    nb = yptr[q];
+    ne = yptr[q + 1];
+    if (hot_row) nh = hot_row[q];
+  };
+  if (wave * G::NSG + sg < R) fetch(wave * G::NSG + sg);
+  for (uint64_t i = wave * G::NSG + sg; i < R; i += stride) {
+    const uint32_t c = nc, hs = nh;
+    const real x = nx;
+    const int64_t b = nb, e = ne;
+    if (i + stride < R) fetch(i + stride);
     uint32_t jj[PP::UT];  // the first pass's columns go out with the finalisation operands
     if (hs == HOT_NONE) PP::load_cols(ycol, b, e, li, jj);
     // col_finalize MODE 1's update part first (it does not depend on the

@@ -2302,6 +2302,15 @@ template <typename real> class Problem final : public ProblemBase {
             done = true;
           }
         }
+        if constexpr (std::is_same<real, double>::value && KP == 32) {
+          if (!no_mfma_) {
+            launch(k_hot_gram_mfma_f64, (unsigned)((own.hchunks.n + 3) / 4), BLOCK, 0, (uint64_t)own.hchunks.n,
+                   (const Job *)own.hchunks.p, (const uint32_t *)own.ycol.p, (const double *)nullptr,
+                   (const double *)h.Q1, (uint64_t)h.partner->R, (double *)hotG_.p, (double *)hotP_.p,
+                   (const double *)nullptr, (const double *)nullptr, 0.0);
+            done = true;
+          }
+        }
         if (!done)
           launch(k_hot_gram<real, KP>, (unsigned)own.hchunks.n, BLOCK, 0, (const Job *)own.hchunks.p,
                  (const uint32_t *)own.ycol.p, (const real *)nullptr, (const real *)h.Q1, hotG_.p, hotP_.p);
@@ -3959,7 +3968,9 @@ template <typename real> class Problem final : public ProblemBase {
   bool sidef_on_ = !std::getenv("OCFFM_SIDE_FULL") || std::atoi(std::getenv("OCFFM_SIDE_FULL")) != 0;
   // OCFFM_XFUSE=0: id-like cross halves' CG steps as k_hs_cross_seg + feature pass instead of k_hv_cross_id
   bool xfuse_on_ = !std::getenv("OCFFM_XFUSE") || std::atoi(std::getenv("OCFFM_XFUSE")) != 0;
-  int xf_gb_ = std::getenv("OCFFM_XF_GB") ? std::atoi(std::getenv("OCFFM_XF_GB")) : 8;  // gathers per round (8 or 16)
+  // gathers per round (8 or 16; fp64 moves half as many rows per round at
+  // the same registers: 16 there, at ~163 registers, 8.72 -> 8.57 ms per epoch)
+  int xf_gb_ = std::getenv("OCFFM_XF_GB") ? std::atoi(std::getenv("OCFFM_XF_GB")) : (sizeof(real) == 8 ? 16 : 8);
   // OCFFM_CGP_COOP=1: cooperative launch (the runtime's residency check; +0.27 ms per kkbox epoch)
   bool cgp_coop_ = std::getenv("OCFFM_CGP_COOP") && std::atoi(std::getenv("OCFFM_CGP_COOP")) != 0;
   // tests: a short spin limit and one block stalled at a given step force the give-up

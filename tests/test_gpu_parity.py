@@ -505,7 +505,7 @@ def test_speculative_update_bit_identical(monkeypatch):
                                  {"OCFFM_SIDE_REFRESH": "1"}, {"OCFFM_SIDE_REFRESH": "0"}, {"OCFFM_TAU_MFMA": "0"},
                                  {"OCFFM_SIDEP": "0"}, {"OCFFM_GFOLD": "0"}, {"OCFFM_SIDE_FULL": "0"},
                                  {"OCFFM_XFUSE": "0"}, {"OCFFM_XF_HOT": "8"}, {"OCFFM_XF_HOT": "100000"},
-                                 {"OCFFM_XF_GB": "16"},
+                                 {"OCFFM_XF_GB": "16"}, {"OCFFM_XF_GB": "8"}, {"OCFFM_NO_MFMA": "1", "OCFFM_XF_HOT": "8"},
                                  {"OCFFM_PGRAM": "2", "OCFFM_CGRAM": "2", "OCFFM_CCG": "2"}])
 def test_execution_variants_fp64(kk_small, monkeypatch, env):
     """Schedule knobs (id-field row fusion, segment length, CG look-ahead)

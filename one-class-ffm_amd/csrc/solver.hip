@@ -1121,7 +1121,7 @@ template <typename real> class Problem final : public ProblemBase {
     ccg_now_ = ccg_eligible(hc) && ccg_mode_ == 2;
     hot_now_ = hot_steps_ == 0;
     col_grams(hc);
-    hot_grams(hc);
+    hot_grams(hc, xfuse(hc));
     // force iteration 1 to run
     CgState hs{};
     hs.run[1] = 1;

@@ -3430,8 +3430,10 @@ template <typename real> class Problem final : public ProblemBase {
         const double rs = sizeof(real);
         DevField<real> &F = *h.F;
         const Fin<real> fin = make_fin(h, it);
-        const double bytes = (double)own.R * (16 + 4 + rs + 4) + (double)(own.npos - own.hpos) * (4 + KP * rs) +
-                             (double)own.nhot * KP * KP * rs + (double)h.D * KP * rs * (it > 1 ? 8 : 3);
+        // (the partner table once, as k_hs_cross_seg's count: its rows are L2 / Infinity Cache hits)
+        const double bytes = (double)own.R * (16 + 4 + rs + 4) + (double)(own.npos - own.hpos) * 4 +
+                             (double)h.partner->R * KP * rs + (double)own.nhot * KP * KP * rs +
+                             (double)h.D * KP * rs * (it > 1 ? 8 : 3);
         auto go = [&](auto gb) {
           constexpr int GB = decltype(gb)::value;
           unsigned grid = grid_for(own.R, 4 * Gm::NSG, hs_blocks_);

@@ -225,7 +225,9 @@ int ocffm_problem_reset_stats(ocffm_problem *p);
  * (SURVEY §8d formula with the actual CG counts). */
 int ocffm_problem_alg_bytes(ocffm_problem *p, double *bytes);
 /* Diagnostic event counters since create (no reference counterpart):
- * "cgp_launches" (persistent column-Gram CG launches), "cgp_recovered"
+ * "cgp_launches" (persistent CG launches: column-Gram and id-like side
+ * halves), "cgp_side_launches" (the latter), "cgp_side_full" (side halves
+ * whose gradient and update ran inside the launch), "cgp_recovered"
  * (launches whose grid gave up on its barrier and whose solve was finished
  * per step), "cgp_refused" (cooperative launches the runtime refused).
  * An unknown name reads 0. */
